@@ -1,0 +1,81 @@
+"""Loader for the in-tree HIP library libfsehip.so (the product).
+
+There is no CPU fallback: if the library is missing or no HIP device is
+usable, calls raise.  Build with ``make -C entropy_coders_amd`` or
+``__graft_entry__.build()``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libfsehip.so")
+
+# every symbol include/fsehip.h declares (checked by tests/test_abi.py)
+EXPORTS = (
+    "fse_compress2", "fse_compress2_log", "fse_decompress2", "histogram_count",
+    "fsehip_slot_bytes", "fsehip_sidecar_per_block", "fsehip_compress_blocks",
+    "fsehip_decompress_blocks", "fsehip_build_sidecar", "fsehip_histogram_blocks",
+    "fsehip_generate", "fsehip_device_count", "fsehip_version",
+)
+
+STATUS = {
+    0: "OK", -1: "EMPTY", -2: "TOO_SHORT", -3: "ALL_ZERO_SYMBOL0", -4: "SINGLE_SYMBOL",
+    -5: "BAD_HEADER", -6: "NO_MARKER", -7: "DST_TOO_SMALL", -8: "TABLELOG_RANGE",
+    -9: "CURSED", -10: "BAD_TABLE", -11: "BAD_ARG", -12: "HIP", -13: "LENGTH_MISMATCH",
+    -14: "UNSUPPORTED", -15: "NO_DEVICE",
+}
+
+
+class FseError(Exception):
+    """A negative status from the C ABI (a reference panic/None/Err)."""
+
+    def __init__(self, rc: int, what: str = ""):
+        self.rc = rc
+        self.code = STATUS.get(rc, str(rc))
+        super().__init__(f"{what}: status {rc} ({self.code})" if what else f"status {rc} ({self.code})")
+
+
+class Params(C.Structure):
+    _fields_ = [("block_size", C.c_uint32), ("table_log", C.c_uint32),
+                ("ckpt_interval", C.c_uint32), ("max_table_log", C.c_uint32)]
+
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: build the HIP extension first "
+                           "(make -C entropy_coders_amd); there is no CPU fallback")
+    lib = C.CDLL(LIB_PATH)
+    P, sz, u32, u64, i32 = C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint64, C.c_int32
+    lib.fse_compress2.argtypes = [P, sz, P, sz, C.POINTER(sz), C.POINTER(u64)]
+    lib.fse_compress2_log.argtypes = [P, sz, u32, P, sz, C.POINTER(sz), C.POINTER(u64)]
+    lib.fse_decompress2.argtypes = [P, sz, P, sz, C.POINTER(sz)]
+    lib.histogram_count.argtypes = [P, sz, P, C.POINTER(u32)]
+    lib.fsehip_slot_bytes.argtypes = [u32, u32]
+    lib.fsehip_slot_bytes.restype = u64
+    lib.fsehip_sidecar_per_block.argtypes = [u32, u32]
+    lib.fsehip_sidecar_per_block.restype = u32
+    lib.fsehip_compress_blocks.argtypes = [C.POINTER(Params), P, u64, P, u64, P, P, P, P, P]
+    lib.fsehip_decompress_blocks.argtypes = [C.POINTER(Params), P, u64, P, P, P, u64, P, P]
+    lib.fsehip_build_sidecar.argtypes = [C.POINTER(Params), P, u64, P, P, u64, P, P, P]
+    lib.fsehip_histogram_blocks.argtypes = [P, u64, u32, P, P, P]
+    lib.fsehip_generate.argtypes = [C.c_int, C.c_double, u64, u32, P, u64, P]
+    lib.fsehip_device_count.argtypes = []
+    lib.fsehip_version.restype = C.c_char_p
+    for name in EXPORTS:
+        if getattr(lib, name, None) is None:
+            raise RuntimeError(f"libfsehip.so lacks {name}")
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        raise FseError(rc, what)

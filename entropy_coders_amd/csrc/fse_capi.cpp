@@ -1,0 +1,317 @@
+// fse_capi.cpp -- C ABI (include/fsehip.h) over the gfx950 kernels.
+//
+// The reference-shaped entry points (fse_compress2, fse_decompress2,
+// histogram_count) stage host buffers through device memory and run the
+// same kernels as the batched API; there is no CPU compute path: without a
+// usable HIP device they return FSE_ERR_NO_DEVICE.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
+#include "../../include/fsehip.h"
+#include "fse_kernels.h"
+
+namespace {
+
+constexpr uint32_t kDefaultBlock = 65536;
+
+uint64_t round_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+
+bool device_ok() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return false;
+    return n > 0;
+}
+
+uint32_t lmax_for(const fsehip_params* p) {
+    if (p->max_table_log) return p->max_table_log;
+    if (p->table_log == 0) return 11;  // optimal_log2 never exceeds 11 (histogram.rs:273-276)
+    return p->table_log < 11 ? 11 : p->table_log;
+}
+
+// Device staging for the host-pointer entry points (grow-only, per thread).
+struct Staging {
+    uint8_t* buf[4] = {nullptr, nullptr, nullptr, nullptr};
+    size_t cap[4] = {0, 0, 0, 0};
+    int device = -1;
+    ~Staging() {
+        for (int i = 0; i < 4; ++i)
+            if (buf[i]) (void)hipFree(buf[i]);
+    }
+    uint8_t* get(int i, size_t bytes) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (dev != device) {
+            for (int j = 0; j < 4; ++j) {
+                if (buf[j]) (void)hipFree(buf[j]);
+                buf[j] = nullptr;
+                cap[j] = 0;
+            }
+            device = dev;
+        }
+        if (cap[i] < bytes) {
+            if (buf[i]) (void)hipFree(buf[i]);
+            buf[i] = nullptr;
+            cap[i] = 0;
+            void* p = nullptr;
+            size_t want = round_up(std::max<size_t>(bytes, 4096), 4096);
+            if (hipMalloc(&p, want) != hipSuccess) return nullptr;
+            buf[i] = static_cast<uint8_t*>(p);
+            cap[i] = want;
+        }
+        return buf[i];
+    }
+};
+thread_local Staging g_stage;
+
+struct Meta {
+    uint32_t comp_len;
+    uint32_t payload_bits;
+    int32_t status;
+    uint32_t pad;
+};
+
+int compress_one(const uint8_t* src, size_t n, uint32_t table_log, uint8_t* dst, size_t dst_cap, size_t* dst_len,
+                 uint64_t* payload_bits) {
+    if (!dst_len) return FSE_ERR_BAD_ARG;
+    if (n == 0) return FSE_ERR_EMPTY;  // size.ilog2() panics (histogram.rs:266)
+    if (n > (1u << 28)) return FSE_ERR_UNSUPPORTED;
+    if (table_log > 12) return FSE_ERR_UNSUPPORTED;
+    if (!device_ok()) return FSE_ERR_NO_DEVICE;
+    fsehip_params p{(uint32_t)round_up(n, 16), table_log, 0, table_log ? std::max<uint32_t>(table_log, 11) : 11};
+    const uint64_t slot = fsehip_slot_bytes(p.block_size, p.max_table_log);
+    uint8_t* d_src = g_stage.get(0, round_up(n, 16) + 16);
+    uint8_t* d_out = g_stage.get(1, slot);
+    uint8_t* d_meta = g_stage.get(2, sizeof(Meta));
+    if (!d_src || !d_out || !d_meta) return FSE_ERR_HIP;
+    if (hipMemcpy(d_src, src, n, hipMemcpyHostToDevice) != hipSuccess) return FSE_ERR_HIP;
+    Meta* m = reinterpret_cast<Meta*>(d_meta);
+    int rc = fsehip_compress_blocks(&p, d_src, n, d_out, slot, &m->comp_len, &m->payload_bits, nullptr,
+                                    &m->status, nullptr);
+    if (rc) return rc;
+    Meta h{};
+    if (hipMemcpy(&h, d_meta, sizeof(Meta), hipMemcpyDeviceToHost) != hipSuccess) return FSE_ERR_HIP;
+    if (h.status != FSE_OK) return h.status;
+    if (*dst_len > dst_cap || dst_cap - *dst_len < h.comp_len) return FSE_ERR_DST_TOO_SMALL;
+    if (hipMemcpy(dst + *dst_len, d_out, h.comp_len, hipMemcpyDeviceToHost) != hipSuccess) return FSE_ERR_HIP;
+    *dst_len += h.comp_len;
+    if (payload_bits) *payload_bits = h.payload_bits;
+    return FSE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint64_t fsehip_slot_bytes(uint32_t block_size, uint32_t max_table_log) {
+    const uint64_t L = max_table_log ? max_table_log : 12;
+    // header <= 512 bytes; every symbol costs <= L bits (fse.rs:170-186);
+    // + both final states and the marker (lib.rs:178-181).
+    const uint64_t payload = ((uint64_t)block_size * L + 2 * L + 1 + 7) / 8;
+    return round_up(512 + payload + 16, 256);
+}
+
+uint32_t fsehip_sidecar_per_block(uint32_t block_size, uint32_t ckpt_interval) {
+    if (ckpt_interval == 0) return 0;
+    return block_size / 2u / ckpt_interval + 2u;
+}
+
+int fsehip_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char* fsehip_version(void) { return "fsehip 0.1 (gfx950)"; }
+
+int fsehip_compress_blocks(const fsehip_params* p, const uint8_t* d_src, uint64_t n_total, uint8_t* d_out,
+                           uint64_t slot_bytes, uint32_t* d_comp_len, uint32_t* d_payload_bits, uint64_t* d_sidecar,
+                           int32_t* d_status, fsehip_stream_t stream) {
+    if (!p || !d_src || !d_out || !d_comp_len || !d_status) return FSE_ERR_BAD_ARG;
+    if (n_total == 0) return FSE_ERR_EMPTY;
+    const uint32_t bs = p->block_size ? p->block_size : kDefaultBlock;
+    const uint64_t n_blocks = (n_total + bs - 1) / bs;
+    if (n_blocks > 1 && (bs & 15u)) return FSE_ERR_BAD_ARG;
+    if (n_blocks > 0xFFFFFFFFull) return FSE_ERR_BAD_ARG;
+    if (p->table_log > 15) return FSE_ERR_TABLELOG_RANGE;
+    const uint32_t lmax = lmax_for(p);
+    if (lmax > 12) return FSE_ERR_UNSUPPORTED;
+    if (slot_bytes & 15u) return FSE_ERR_BAD_ARG;
+    if (p->ckpt_interval && (p->ckpt_interval < 8 || (p->ckpt_interval & (p->ckpt_interval - 1)))) return FSE_ERR_BAD_ARG;
+    if (!device_ok()) return FSE_ERR_NO_DEVICE;
+    fsehip::EncParams P{};
+    P.src = d_src;
+    P.n_total = n_total;
+    P.block_size = bs;
+    P.n_blocks = (uint32_t)n_blocks;
+    P.table_log = p->table_log;
+    P.ckpt_interval = d_sidecar ? p->ckpt_interval : 0;
+    P.ckpt_per_block = fsehip_sidecar_per_block(bs, P.ckpt_interval);
+    P.out = d_out;
+    P.slot_bytes = slot_bytes;
+    P.comp_len = d_comp_len;
+    P.payload_bits = d_payload_bits;
+    P.sidecar = P.ckpt_interval ? d_sidecar : nullptr;
+    P.status = d_status;
+    hipError_t e = fsehip::launch_encode(P, lmax, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? FSE_OK : FSE_ERR_HIP;
+}
+
+static int decompress_impl(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
+                           const uint32_t* d_comp_len, const uint64_t* d_sidecar, uint8_t* d_out, uint64_t n_total,
+                           uint64_t* d_sidecar_out, int32_t* d_status, uint32_t* d_out_len, uint32_t out_cap,
+                           fsehip_stream_t stream) {
+    if (!p || !d_in || !d_comp_len || !d_out || !d_status) return FSE_ERR_BAD_ARG;
+    const uint32_t bs = p->block_size ? p->block_size : kDefaultBlock;
+    const uint64_t n_blocks = n_total ? (n_total + bs - 1) / bs : 1;
+    if (n_blocks > 1 && (bs & 15u)) return FSE_ERR_BAD_ARG;
+    if (slot_bytes & 3u) return FSE_ERR_BAD_ARG;
+    if ((d_sidecar || d_sidecar_out) &&
+        (p->ckpt_interval < 8 || (p->ckpt_interval & (p->ckpt_interval - 1))))
+        return FSE_ERR_BAD_ARG;
+    if (!device_ok()) return FSE_ERR_NO_DEVICE;
+    fsehip::DecParams P{};
+    P.in = d_in;
+    P.slot_bytes = slot_bytes;
+    P.comp_len = d_comp_len;
+    P.sidecar = d_sidecar;
+    P.ckpt_interval = p->ckpt_interval;
+    P.ckpt_per_block = fsehip_sidecar_per_block(bs, p->ckpt_interval);
+    P.out = d_out;
+    P.n_total = n_total;
+    P.block_size = bs;
+    P.n_blocks = (uint32_t)n_blocks;
+    P.out_cap = out_cap;
+    P.status = d_status;
+    P.out_len = d_out_len;
+    P.sidecar_out = d_sidecar_out;
+    // the decoder reads L from each header; size its tables for the bound
+    uint32_t lmax = p->max_table_log ? p->max_table_log : 12;
+    hipError_t e = fsehip::launch_decode(P, lmax, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? FSE_OK : FSE_ERR_HIP;
+}
+
+int fsehip_decompress_blocks(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
+                             const uint32_t* d_comp_len, const uint64_t* d_sidecar, uint8_t* d_out, uint64_t n_total,
+                             int32_t* d_status, fsehip_stream_t stream) {
+    if (n_total == 0) return FSE_ERR_EMPTY;
+    if (d_sidecar && p && p->ckpt_interval == 0) return FSE_ERR_BAD_ARG;
+    return decompress_impl(p, d_in, slot_bytes, d_comp_len, d_sidecar, d_out, n_total, nullptr, d_status, nullptr,
+                           0, stream);
+}
+
+int fsehip_build_sidecar(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
+                         const uint32_t* d_comp_len, uint8_t* d_out, uint64_t n_total, uint64_t* d_sidecar_out,
+                         int32_t* d_status, fsehip_stream_t stream) {
+    if (n_total == 0) return FSE_ERR_EMPTY;
+    return decompress_impl(p, d_in, slot_bytes, d_comp_len, nullptr, d_out, n_total, d_sidecar_out, d_status,
+                           nullptr, 0, stream);
+}
+
+int fsehip_histogram_blocks(const uint8_t* d_src, uint64_t n_total, uint32_t block_size, uint32_t* d_counts,
+                            uint32_t* d_table_len, fsehip_stream_t stream) {
+    if (!d_src || !d_counts) return FSE_ERR_BAD_ARG;
+    const uint32_t bs = block_size ? block_size : kDefaultBlock;
+    const uint64_t n_blocks = n_total ? (n_total + bs - 1) / bs : 1;
+    if (n_blocks > 1 && (bs & 15u)) return FSE_ERR_BAD_ARG;
+    if (!device_ok()) return FSE_ERR_NO_DEVICE;
+    hipError_t e = fsehip::launch_histogram(d_src, n_total, bs, (uint32_t)n_blocks, d_counts, d_table_len,
+                                            static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? FSE_OK : FSE_ERR_HIP;
+}
+
+int fsehip_generate(int kind, double prob, uint64_t seed, uint32_t block_size, uint8_t* d_out, uint64_t n_total,
+                    fsehip_stream_t stream) {
+    if (!d_out || kind < 0 || kind > 2) return FSE_ERR_BAD_ARG;
+    if (n_total == 0) return FSE_OK;
+    if (!device_ok()) return FSE_ERR_NO_DEVICE;
+    fsehip::GenParams G{};
+    G.out = d_out;
+    G.n_total = n_total;
+    G.block_size = block_size ? block_size : kDefaultBlock;
+    G.seed = seed;
+    G.kind = kind;
+    if (kind == 0) {
+        // LUT of benches/fse_benchmark.rs:5-20 as symbol start indices
+        if (prob < 0.005) prob = 0.005;
+        if (prob > 0.995) prob = 0.995;
+        size_t remaining = 4096, idx = 0;
+        uint32_t s = 0;
+        while (remaining > 0) {
+            size_t cnt = (size_t)((double)remaining * prob);
+            if (cnt < 1) cnt = 1;
+            if (s >= 1024) return FSE_ERR_BAD_ARG;
+            G.bound[s++] = (uint16_t)idx;
+            idx += cnt;
+            remaining -= cnt;
+        }
+        G.nsym = s;
+    }
+    hipError_t e = fsehip::launch_generate(G, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? FSE_OK : FSE_ERR_HIP;
+}
+
+// ---------------------------------------------------------------- host API
+
+int fse_compress2(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, size_t* dst_len,
+                  uint64_t* payload_bits) {
+    return compress_one(src, n, 0, dst, dst_cap, dst_len, payload_bits);
+}
+
+int fse_compress2_log(const uint8_t* src, size_t n, uint32_t table_log, uint8_t* dst, size_t dst_cap,
+                      size_t* dst_len, uint64_t* payload_bits) {
+    if (table_log == 0) return FSE_ERR_TABLELOG_RANGE;
+    return compress_one(src, n, table_log, dst, dst_cap, dst_len, payload_bits);
+}
+
+int fse_decompress2(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, size_t* dst_len) {
+    if (!dst_len || *dst_len > dst_cap) return FSE_ERR_BAD_ARG;
+    if (n == 0) return FSE_ERR_EMPTY;  // BitStreamReader::new asserts (stream_reader.rs:17)
+    if (n > (1u << 30)) return FSE_ERR_UNSUPPORTED;
+    if (!device_ok()) return FSE_ERR_NO_DEVICE;
+    const uint64_t padded = round_up(n, 16) + 16;
+    const uint64_t cap64 = std::min<uint64_t>(dst_cap - *dst_len, 0x7FFFFFFFu);
+    uint8_t* d_in = g_stage.get(0, padded);
+    uint8_t* d_out = g_stage.get(1, std::max<uint64_t>(cap64, 16));
+    uint8_t* d_meta = g_stage.get(2, sizeof(Meta));
+    if (!d_in || !d_out || !d_meta) return FSE_ERR_HIP;
+    if (hipMemset(d_in, 0, padded) != hipSuccess) return FSE_ERR_HIP;
+    if (hipMemcpy(d_in, src, n, hipMemcpyHostToDevice) != hipSuccess) return FSE_ERR_HIP;
+    Meta* m = reinterpret_cast<Meta*>(d_meta);
+    Meta h0{(uint32_t)n, 0, 0, 0};
+    if (hipMemcpy(d_meta, &h0, sizeof(Meta), hipMemcpyHostToDevice) != hipSuccess) return FSE_ERR_HIP;
+    fsehip_params p{0, 0, 0, 12};
+    int rc = decompress_impl(&p, d_in, padded, &m->comp_len, nullptr, d_out, 0, nullptr, &m->status,
+                             &m->payload_bits, (uint32_t)cap64, nullptr);
+    if (rc) return rc;
+    Meta h{};
+    if (hipMemcpy(&h, d_meta, sizeof(Meta), hipMemcpyDeviceToHost) != hipSuccess) return FSE_ERR_HIP;
+    if (h.status != FSE_OK) return h.status;
+    const uint32_t out_len = h.payload_bits;  // decoded byte count
+    if (out_len && hipMemcpy(dst + *dst_len, d_out, out_len, hipMemcpyDeviceToHost) != hipSuccess) return FSE_ERR_HIP;
+    *dst_len += out_len;
+    return FSE_OK;
+}
+
+int histogram_count(const uint8_t* src, size_t n, uint32_t counts[256], uint32_t* table_len) {
+    if (!counts) return FSE_ERR_BAD_ARG;
+    if (n > 0xFFFFFFFFull) return FSE_ERR_BAD_ARG;  // histogram.rs:19 assert
+    if (!device_ok()) return FSE_ERR_NO_DEVICE;
+    uint8_t* d_src = g_stage.get(0, round_up(n, 16) + 16);
+    uint8_t* d_cnt = g_stage.get(2, 257 * 4);
+    if (!d_src || !d_cnt) return FSE_ERR_HIP;
+    if (n && hipMemcpy(d_src, src, n, hipMemcpyHostToDevice) != hipSuccess) return FSE_ERR_HIP;
+    uint32_t* c = reinterpret_cast<uint32_t*>(d_cnt);
+    hipError_t e = fsehip::launch_histogram(d_src, n, (uint32_t)std::max<size_t>(n, 1), 1, c, c + 256, nullptr);
+    if (e != hipSuccess) return FSE_ERR_HIP;
+    uint32_t h[257];
+    if (hipMemcpy(h, d_cnt, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess) return FSE_ERR_HIP;
+    memcpy(counts, h, 256 * sizeof(uint32_t));
+    if (table_len) *table_len = h[256];
+    return FSE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,506 @@
+// fse_device.hpp -- CDNA4 (gfx950) device building blocks of the FSE coder.
+//
+// Everything here runs inside one 64-lane wavefront: statistics, the
+// normalised histogram, the NCount header and the tANS tables are produced
+// by a single wave per block with LDS scratch, so kernels need no
+// cross-wave synchronisation.  Each function cites the reference
+// (Cognoscan/entropy_coders) lines whose behaviour it reproduces bit-exactly.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/fse_status.h"
+
+namespace fsehip {
+
+constexpr uint32_t LOG_MIN = 5;       // lib.rs:9
+constexpr uint32_t LOG_MAX_REF = 15;  // lib.rs:10
+constexpr uint32_t LOG_DEFAULT = 11;  // lib.rs:12
+constexpr uint32_t HDR_MAX = 512;     // header bytes kept in LDS
+constexpr uint32_t WAVE = 64;
+
+__device__ __forceinline__ uint32_t ilog2u(uint32_t x) { return 31u - (uint32_t)__clz(x); }
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+__device__ __forceinline__ uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
+
+// Inclusive prefix sum across the wave (6 DPP-able shuffle steps).
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t o = __shfl_up(v, d, 64);
+        if ((int)lane_id() >= d) v += o;
+    }
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = max(v, (uint32_t)__shfl_xor(v, d, 64));
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t o = __shfl_up(v, d, 64);
+        if ((int)lane_id() >= d) v = max(v, o);
+    }
+    return v;
+}
+
+// Lanes of the wave holding the same 8-bit key (8 ballots), restricted to
+// the active lanes.
+__device__ __forceinline__ uint64_t match_u8(uint32_t key, uint64_t active) {
+    uint64_t peers = active;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        uint64_t bal = __ballot((key >> b) & 1u);
+        peers &= ((key >> b) & 1u) ? bal : ~bal;
+    }
+    return peers;
+}
+
+// ---------------------------------------------------------------------------
+// Histogram::new (histogram.rs:18-66): 256-bin count of one block by one
+// wave; four LDS sub-histograms (lane & 3) spread same-symbol atomics.
+// Returns table_len (1 + largest symbol, 1 for an empty block).
+// ---------------------------------------------------------------------------
+__device__ inline uint32_t wave_histogram(const uint8_t* __restrict__ src, uint32_t n,
+                                          uint32_t* h4 /*LDS [4][256]*/, uint32_t* counts /*LDS[256]*/) {
+    const uint32_t lane = lane_id();
+    for (uint32_t i = lane; i < 1024; i += WAVE) h4[i] = 0;
+    __syncthreads();
+    uint32_t* mine = h4 + (lane & 3u) * 256u;
+    uint32_t done = 0;
+    if ((reinterpret_cast<uintptr_t>(src) & 15u) == 0) {
+        const uint32_t nvec = n >> 4;
+        const uint4* v4 = reinterpret_cast<const uint4*>(src);
+        for (uint32_t v = lane; v < nvec; v += WAVE) {
+            uint4 d = v4[v];
+            uint32_t w[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+#pragma unroll
+                for (int b = 0; b < 4; ++b) atomicAdd(&mine[(w[k] >> (8 * b)) & 0xFFu], 1u);
+            }
+        }
+        done = nvec << 4;
+    }
+    for (uint32_t i = done + lane; i < n; i += WAVE) atomicAdd(&mine[src[i]], 1u);
+    __syncthreads();
+    uint32_t tl = 0;
+    for (uint32_t s = lane; s < 256; s += WAVE) {
+        uint32_t c = h4[s] + h4[256 + s] + h4[512 + s] + h4[768 + s];
+        counts[s] = c;
+        if (c) tl = max(tl, s + 1u);
+    }
+    tl = wave_max(tl);
+    __syncthreads();
+    return tl == 0 ? 1u : tl;
+}
+
+// ---------------------------------------------------------------------------
+// optimal_log2 (histogram.rs:264-277), release-build u32 semantics.
+// ---------------------------------------------------------------------------
+__device__ inline int optimal_log2(uint32_t size, uint32_t table_len, uint32_t* L) {
+    if (size == 0) return FSE_ERR_EMPTY;
+    uint32_t min_src = ilog2u(size) + 1u;
+    if (table_len <= 1) return FSE_ERR_ALL_ZERO_SYMBOL0;
+    uint32_t min_sym = ilog2u(table_len - 1u) + 2u;
+    uint32_t min_bits = min(min_src, min_sym);
+    if (size == 1) return FSE_ERR_TOO_SHORT;
+    uint32_t max_bits = ilog2u(size - 1u) - 2u;  // wraps for size 2..4
+    uint32_t r = max(min(LOG_DEFAULT, max_bits), min_bits);
+    r = min(max(r, LOG_MIN), LOG_MAX_REF);
+    *L = r;
+    return FSE_OK;
+}
+
+constexpr int32_t UNASSIGNED = -2;
+
+// normalize_slow (histogram.rs:157-261): rare, single lane.
+__device__ inline int normalize_slow_lane(const uint32_t* counts, uint32_t size, uint32_t tl, uint32_t L,
+                                          int32_t* norm) {
+    uint32_t low_t = size >> L;
+    uint32_t low_one = (uint32_t)(size * 3u) >> (L + 1u);
+    uint32_t td = 1u << L;
+    uint32_t total = size;
+    for (uint32_t s = 0; s < 256; ++s) norm[s] = 0;
+    for (uint32_t s = 0; s < tl; ++s) {
+        uint32_t t = counts[s];
+        if (t == 0) continue;
+        if (t <= low_t) { norm[s] = -1; td -= 1; total -= t; }
+        else if (t <= low_one) { norm[s] = 1; td -= 1; total -= t; }
+        else norm[s] = UNASSIGNED;
+    }
+    if (td == 0) return FSE_OK;
+    if (total / td > low_one) {
+        uint32_t low = (uint32_t)(total * 3u) / (uint32_t)(td * 2u);
+        for (uint32_t s = 0; s < tl; ++s)
+            if (norm[s] == UNASSIGNED && counts[s] <= low) { norm[s] = 1; td -= 1; total -= counts[s]; }
+    }
+    if ((uint32_t)((1u << L) - td) == tl) {
+        uint32_t vmax = 0, imax = 0;
+        for (uint32_t s = 0; s < 256; ++s)
+            if (counts[s] > vmax) { vmax = counts[s]; imax = s; }
+        norm[imax] += (int32_t)td;
+        return FSE_OK;
+    }
+    if (total == 0) {
+        while (td != 0) {
+            bool moved = false;
+            for (uint32_t s = 0; s < tl; ++s) {
+                if (norm[s] > 0) {
+                    norm[s] += 1; td -= 1; moved = true;
+                    if (td == 0) break;
+                }
+            }
+            if (!moved) return FSE_ERR_CURSED;
+        }
+        return FSE_OK;
+    }
+    const uint32_t vsl = 62u - L;
+    const uint64_t mid = (1ull << (vsl - 1u)) - 1ull;
+    const uint64_t r_step = (((1ull << vsl) * (uint64_t)td) + mid) / (uint64_t)total;
+    uint64_t acc = mid;
+    for (uint32_t s = 0; s < tl; ++s) {
+        if (norm[s] == UNASSIGNED) {
+            uint64_t end = acc + (uint64_t)counts[s] * r_step;
+            uint64_t w = (end >> vsl) - (acc >> vsl);
+            if (w < 1) return FSE_ERR_CURSED;
+            norm[s] = (int32_t)w;
+            acc = end;
+        }
+    }
+    return FSE_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Histogram::normalize (histogram.rs:95-155), wave-parallel fast path: each
+// lane owns 4 symbols; the residual goes to the first largest symbol (strict
+// `>` at 135) found by a (prob, -index) max-reduction; the slow path runs on
+// lane 0.  Returns status; *L_out = effective tableLog.
+// ---------------------------------------------------------------------------
+__device__ inline int wave_normalize(const uint32_t* counts, uint32_t size, uint32_t tl, uint32_t log2_req,
+                                     int32_t* norm, uint32_t* L_out, uint32_t* used_slow, int* scratch) {
+    const uint32_t lane = lane_id();
+    if (tl <= 1) return FSE_ERR_ALL_ZERO_SYMBOL0;  // ilog2(0) at 98
+    if (size == 0) return FSE_ERR_EMPTY;
+    uint32_t L = min(max(log2_req, LOG_MIN), LOG_MAX_REF);
+    L = max(L, ilog2u(tl - 1u) + 2u);
+    const uint32_t scale = 62u - L;
+    const uint64_t step = (1ull << 62) / (uint64_t)size;
+    const uint64_t v_step = 1ull << (scale - 20u);
+    const uint32_t low_t = size >> L;
+    const uint32_t RTB[8] = {0, 473195, 504333, 520860, 550000, 700000, 750000, 830000};
+
+    uint32_t local_sum = 0, best = 0, single = 0;
+    for (uint32_t k = 0; k < 4; ++k) {
+        uint32_t s = lane * 4u + k;
+        int32_t v = 0;
+        if (s < tl) {
+            uint32_t t = counts[s];
+            if (t == size) {
+                single = s + 1u;
+            } else if (t == 0) {
+                v = 0;
+            } else if (t <= low_t) {
+                v = -1;
+                local_sum += 1;
+            } else {
+                uint64_t p = ((uint64_t)t * step) >> scale;
+                if (p < 8) p += (((uint64_t)t * step - (p << scale)) > v_step * (uint64_t)RTB[p]) ? 1u : 0u;
+                v = (int32_t)p;
+                local_sum += (uint32_t)p;
+                uint32_t key = ((uint32_t)p << 8) | (255u - s);
+                if (p > 0) best = max(best, key);
+            }
+        }
+        norm[s] = v;
+    }
+    single = wave_max(single);
+    uint32_t sum = wave_sum(local_sum);
+    best = wave_max(best);
+    *used_slow = 0;
+    if (single) {  // t == size returns immediately (113-120); other counts are 0
+        if (lane == 0) norm[single - 1u] = (int32_t)(1u << L);
+        __syncthreads();
+        *L_out = L;
+        return FSE_OK;
+    }
+    const int32_t to_distribute = (int32_t)(1u << L) - (int32_t)sum;
+    const int32_t largest_prob = (int32_t)(best >> 8);
+    const uint32_t largest = best ? 255u - (best & 255u) : 0u;
+    __syncthreads();
+    int rc = FSE_OK;
+    if (to_distribute != 0 && -to_distribute >= (largest_prob >> 1)) {
+        *used_slow = 1;
+        if (lane == 0) scratch[0] = normalize_slow_lane(counts, size, tl, L, norm);
+        __syncthreads();
+        rc = scratch[0];
+    } else {
+        if (lane == 0) norm[largest] += to_distribute;
+    }
+    __syncthreads();
+    *L_out = L;
+    return rc;
+}
+
+// ---------------------------------------------------------------------------
+// NormHistogram::write (histogram.rs:376-431), one lane.  Writes the header
+// bytes into hdr[] (LDS) and returns the byte length (<= HDR_MAX) or < 0.
+// ---------------------------------------------------------------------------
+struct ByteWriter {
+    uint8_t* buf;
+    uint32_t byte;
+    uint64_t acc;
+    uint32_t nacc;
+    bool overflow;
+    __device__ void put(uint32_t v, uint32_t nb) {
+        acc |= (uint64_t)(v & ((1u << nb) - 1u)) << nacc;
+        nacc += nb;
+        while (nacc >= 8) {
+            if (byte < HDR_MAX) buf[byte] = (uint8_t)acc; else overflow = true;
+            byte++;
+            acc >>= 8;
+            nacc -= 8;
+        }
+    }
+    __device__ uint32_t finish() {
+        if (nacc) {
+            if (byte < HDR_MAX) buf[byte] = (uint8_t)acc; else overflow = true;
+            byte++;
+        }
+        return byte;
+    }
+};
+
+__device__ inline int header_write_lane(const int32_t* norm, uint32_t L, uint32_t tl, uint8_t* hdr) {
+    ByteWriter w{hdr, 0, 0, 0, false};
+    w.put(L - LOG_MIN, 4);
+    int32_t thr = 1 << L;
+    int32_t rem = thr + 1;
+    uint32_t zc = 0;
+    uint32_t nb = L + 1u;
+    for (uint32_t i = 0; i < tl; ++i) {
+        int32_t s = norm[i];
+        if (rem <= 1) break;
+        if (zc != 0) {
+            if (s == 0) { zc += 1; continue; }
+            zc -= 1;
+            while (zc >= 24) { w.put(0xFFFF, 16); zc -= 24; }
+            while (zc >= 3) { w.put(3, 2); zc -= 3; }
+            w.put(zc, 2);
+        }
+        int32_t mx = (2 * thr - 1) - rem;
+        rem -= (s < 0 ? -s : s);
+        int32_t c = s + 1;
+        if (c >= thr) c += mx;
+        w.put((uint32_t)c, nb - (c < mx ? 1u : 0u));
+        zc = (c == 1) ? 1u : 0u;
+        if (rem < 1) return FSE_ERR_BAD_TABLE;
+        while (rem < thr) { nb -= 1; thr >>= 1; }
+    }
+    uint32_t len = w.finish();
+    if (w.overflow) return FSE_ERR_DST_TOO_SMALL;
+    return (int)len;
+}
+
+// ---------------------------------------------------------------------------
+// NormHistogram::read (histogram.rs:436-505) + BitStreamReader semantics
+// (stream_reader.rs:16-135), one lane, reading global memory.  Returns the
+// consumed byte count (finish_byte) or < 0.
+// ---------------------------------------------------------------------------
+struct FwdReader {
+    const uint8_t* buf;
+    uint32_t total;  // bits
+    uint32_t pos;
+    __device__ bool peek(uint32_t nb, uint32_t* v) const {
+        if (pos + nb > total) return false;
+        uint32_t b = pos >> 3, sh = pos & 7u;
+        uint64_t w = 0;
+        uint32_t nbytes = (sh + nb + 7u) >> 3;
+        for (uint32_t i = 0; i < nbytes; ++i)
+            if (b + i < (total >> 3)) w |= (uint64_t)buf[b + i] << (8u * i);
+        *v = (uint32_t)((w >> sh) & ((1ull << nb) - 1ull));
+        return true;
+    }
+    __device__ bool advance(uint32_t nb) {
+        if (pos + nb > total) return false;
+        pos += nb;
+        return true;
+    }
+};
+
+__device__ inline int header_read_lane(const uint8_t* src, uint32_t n, int32_t* norm, uint32_t* L_out,
+                                       uint32_t* tl_out) {
+    if (n == 0) return FSE_ERR_EMPTY;
+    FwdReader r{src, n * 8u, 0};
+    uint32_t v;
+    if (!r.peek(4, &v)) return FSE_ERR_BAD_HEADER;
+    r.advance(4);
+    const uint32_t L = v + LOG_MIN;
+    if (L > LOG_MAX_REF) return FSE_ERR_BAD_HEADER;
+    for (uint32_t s = 0; s < 256; ++s) norm[s] = 0;
+    uint32_t sym = 0;
+    uint32_t thr = 1u << L;
+    uint32_t rem = thr + 1u;
+    uint32_t nb = L + 1u;
+    bool prev0 = false;
+    while (rem > 1 && sym < 256) {
+        if (prev0) {
+            for (;;) {
+                uint32_t pk;
+                if (!r.peek(16, &pk)) pk = 0;
+                if (pk != 0xFFFFu) break;
+                if (!r.advance(16)) return FSE_ERR_BAD_HEADER;
+                sym += 24;
+            }
+            for (;;) {
+                uint32_t pk;
+                if (!r.peek(2, &pk)) pk = 0;
+                if (pk != 3u) break;
+                if (!r.advance(2)) return FSE_ERR_BAD_HEADER;
+                sym += 3;
+            }
+            if (!r.peek(2, &v)) return FSE_ERR_BAD_HEADER;
+            r.advance(2);
+            sym += v;
+        }
+        if (sym >= 256) break;
+        const uint32_t mx = (2u * thr - 1u) - rem;
+        uint32_t raw;
+        if (!r.peek(nb, &raw) && !r.peek(nb - 1u, &raw)) return FSE_ERR_BAD_HEADER;
+        uint32_t val;
+        if ((raw & (thr - 1u)) < mx) {
+            if (!r.advance(nb - 1u)) return FSE_ERR_BAD_HEADER;
+            val = raw & (thr - 1u);
+        } else {
+            if (!r.advance(nb)) return FSE_ERR_BAD_HEADER;
+            val = raw & (2u * thr - 1u);
+            if (val >= thr) val -= mx;
+        }
+        int32_t sv = (int32_t)val - 1;
+        rem -= (uint32_t)(sv < 0 ? -sv : sv);
+        norm[sym] = sv;
+        sym += 1;
+        prev0 = (sv == 0);
+        while (rem < thr) { nb -= 1; thr >>= 1; }
+    }
+    if (rem != 1) return FSE_ERR_BAD_HEADER;
+    *L_out = L;
+    *tl_out = sym;
+    return (int)((r.pos + 7u) >> 3);
+}
+
+// ---------------------------------------------------------------------------
+// Symbol spread and per-position occurrence rank (fse.rs:110-162, 294-337),
+// wave-parallel.  After the call:
+//   sym_at[i]  = symbol at table position i            (LDS, 2^L bytes)
+//   cumul[s]   = sum_{t<s} c'(t), c' = 1 for -1         (LDS, 256)
+// and `visit(i, s, rank)` is invoked once per position with the rank of
+// position i among the positions holding s in ascending position order
+// (stateTable order, fse.rs:158-162; DecodeTable order, fse.rs:329-337).
+//
+// The spread walks multipliers m = 0..2^L-1: position (m*step) mod 2^L is
+// visited iff it is <= the high threshold, and the j-th visited position
+// gets the j-th positive occurrence in symbol order (fse.rs:139-150).  The
+// owner of occurrence j comes from a forward max-fill of symbol start marks.
+// Ranks come from 8-ballot peer matching over 64 consecutive positions plus
+// running per-symbol counters.
+// ---------------------------------------------------------------------------
+template <typename Visit>
+__device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_t tl, uint8_t* sym_at,
+                                        uint8_t* occ_sym, uint16_t* cumul, uint32_t* cnt, Visit visit) {
+    const uint32_t lane = lane_id();
+    const uint32_t size = 1u << L;
+    const uint32_t mask = size - 1u;
+    // per-lane 4 symbols: c'(s), positive count, -1 flag
+    uint32_t cp[4], pos_n[4], neg[4];
+    uint32_t sum_c = 0, sum_p = 0, sum_neg = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        uint32_t s = lane * 4u + k;
+        int32_t v = (s < tl) ? norm[s] : 0;
+        neg[k] = (v == -1 || v < -1) ? 1u : 0u;
+        pos_n[k] = v > 0 ? (uint32_t)v : 0u;
+        cp[k] = (v == -1) ? 1u : pos_n[k];
+        sum_c += cp[k];
+        sum_p += pos_n[k];
+        sum_neg += neg[k];
+    }
+    const uint32_t ex_c = wave_incl_sum(sum_c) - sum_c;
+    const uint32_t ex_p = wave_incl_sum(sum_p) - sum_p;
+    const uint32_t ex_n = wave_incl_sum(sum_neg) - sum_neg;
+    const uint32_t total_neg = __shfl(ex_n + sum_neg, 63, 64);
+    const uint32_t total_pos = __shfl(ex_p + sum_p, 63, 64);
+    if (total_pos + total_neg > size || total_neg > size) return FSE_ERR_BAD_TABLE;
+    const int32_t ht = (int32_t)size - 1 - (int32_t)total_neg;
+    for (uint32_t i = lane; i < size; i += WAVE) { occ_sym[i] = 0; sym_at[i] = 0; }
+    for (uint32_t s = lane; s < 256; s += WAVE) cnt[s] = 0;
+    __syncthreads();
+    {
+        uint32_t c = ex_c, p = ex_p, ng = ex_n;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            uint32_t s = lane * 4u + k;
+            cumul[s] = (uint16_t)c;
+            if (pos_n[k]) occ_sym[p] = (uint8_t)s;  // start mark of s's occurrences
+            if (neg[k]) sym_at[size - 1u - ng] = (uint8_t)s;  // -1 symbols from the top (122-125)
+            c += cp[k];
+            p += pos_n[k];
+            ng += neg[k];
+        }
+    }
+    __syncthreads();
+    // forward max-fill: occ_sym[j] = owner of positive occurrence j
+    {
+        uint32_t carry = 0;
+        for (uint32_t base = 0; base < total_pos; base += WAVE) {
+            uint32_t j = base + lane;
+            uint32_t v = (j < total_pos) ? occ_sym[j] : 0u;
+            uint32_t f = max(wave_incl_max(v), carry);
+            if (j < total_pos) occ_sym[j] = (uint8_t)f;
+            carry = __shfl(f, 63, 64);
+        }
+    }
+    __syncthreads();
+    // spread: j-th valid multiplier -> position
+    const uint32_t step = (size >> 3) * 5u + 3u;  // table_step: size*5/8+3 (fse.rs:67-70)
+    {
+        uint32_t j0 = 0;
+        for (uint32_t base = 0; base < size; base += WAVE) {
+            uint32_t m = base + lane;
+            bool act = m < size;
+            uint32_t p = (m * step) & mask;
+            bool valid = act && (int32_t)p <= ht;
+            uint64_t bal = __ballot(valid);
+            uint32_t j = j0 + (uint32_t)__popcll(bal & lanemask_lt());
+            if (valid && j < total_pos) sym_at[p] = occ_sym[j];
+            j0 += (uint32_t)__popcll(bal);
+        }
+        if (j0 != total_pos) return FSE_ERR_BAD_TABLE;  // position != 0 assert
+    }
+    __syncthreads();
+    // occurrence ranks in ascending position order
+    for (uint32_t base = 0; base < size; base += WAVE) {
+        uint32_t i = base + lane;
+        bool act = i < size;
+        uint64_t active = __ballot(act);
+        uint32_t s = act ? sym_at[i] : 0u;
+        uint64_t peers = match_u8(s, active);
+        uint32_t before = act ? cnt[s] : 0u;
+        uint32_t r = before + (uint32_t)__popcll(peers & lanemask_lt());
+        __syncthreads();
+        bool leader = act && ((peers & lanemask_lt()) == 0);
+        if (leader) cnt[s] = before + (uint32_t)__popcll(peers);
+        if (act) visit(i, s, r);
+        __syncthreads();
+    }
+    return FSE_OK;
+}
+
+}  // namespace fsehip

@@ -1,0 +1,58 @@
+// fse_kernels.h -- internal launch interface between the C ABI (fse_capi.cpp)
+// and the gfx950 kernels (fse_kernels.hip).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fsehip {
+
+struct EncParams {
+    const uint8_t* src;
+    uint64_t n_total;
+    uint32_t block_size;
+    uint32_t n_blocks;
+    uint32_t table_log;      // 0 = NormHistogram::new (optimal_log2)
+    uint32_t ckpt_interval;  // pairs between sidecar checkpoints (power of 2) or 0
+    uint32_t ckpt_per_block; // sidecar entries reserved per block
+    uint8_t* out;            // n_blocks * slot_bytes
+    uint64_t slot_bytes;
+    uint32_t* comp_len;
+    uint32_t* payload_bits;
+    uint64_t* sidecar;
+    int32_t* status;
+};
+
+struct DecParams {
+    const uint8_t* in;
+    uint64_t slot_bytes;
+    const uint32_t* comp_len;
+    const uint64_t* sidecar;  // nullptr -> serial reference-mode decode
+    uint32_t ckpt_interval;
+    uint32_t ckpt_per_block;
+    uint8_t* out;
+    uint64_t n_total;  // 0 -> raw length unknown (reference mode, out_cap bytes)
+    uint32_t block_size;
+    uint32_t n_blocks;
+    uint32_t out_cap;
+    int32_t* status;
+    uint32_t* out_len;
+    uint64_t* sidecar_out;  // serial mode: record checkpoints here
+};
+
+struct GenParams {
+    uint8_t* out;
+    uint64_t n_total;
+    uint64_t block_size;
+    uint64_t seed;
+    int32_t kind;
+    uint32_t nsym;
+    uint16_t bound[1024];
+};
+
+hipError_t launch_encode(const EncParams& P, uint32_t lmax, hipStream_t stream);
+hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream);
+hipError_t launch_histogram(const uint8_t* src, uint64_t n_total, uint32_t block_size, uint32_t n_blocks,
+                            uint32_t* counts, uint32_t* table_len, hipStream_t stream);
+hipError_t launch_generate(const GenParams& G, hipStream_t stream);
+
+}  // namespace fsehip

@@ -1,0 +1,159 @@
+"""Python mirror of the reference crate's API for this path (tests, bench).
+
+Reference-shaped calls (host bytes in, bytes out; lib.rs:146-248,
+histogram.rs:18-66) and a batched device codec over torch tensors.  All
+compute goes through libfsehip.so on the GPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._lib import FseError, Params, check, load
+
+
+def _buf(data) -> np.ndarray:
+    if isinstance(data, np.ndarray):
+        return np.ascontiguousarray(data, dtype=np.uint8)
+    return np.frombuffer(bytes(data), dtype=np.uint8)
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def compress2(src) -> tuple[bytes, int]:
+    """`fse_compress2(src, &mut dst) -> usize` (lib.rs:146): (bytes, payload bits)."""
+    a = _buf(src)
+    lib = load()
+    cap = int(lib.fsehip_slot_bytes(max(len(a), 16), 12))
+    dst = np.zeros(cap, dtype=np.uint8)
+    n = C.c_size_t(0)
+    bits = C.c_uint64(0)
+    check(lib.fse_compress2(_p(a), len(a), _p(dst), cap, C.byref(n), C.byref(bits)), "fse_compress2")
+    return dst[: n.value].tobytes(), bits.value
+
+
+def compress2_log(src, table_log: int) -> tuple[bytes, int]:
+    """`Histogram::new(src).normalize(L)` + fse_compress2 body (histogram.rs:95)."""
+    a = _buf(src)
+    lib = load()
+    cap = int(lib.fsehip_slot_bytes(max(len(a), 16), 12))
+    dst = np.zeros(cap, dtype=np.uint8)
+    n = C.c_size_t(0)
+    bits = C.c_uint64(0)
+    check(lib.fse_compress2_log(_p(a), len(a), table_log, _p(dst), cap, C.byref(n), C.byref(bits)),
+          "fse_compress2_log")
+    return dst[: n.value].tobytes(), bits.value
+
+
+def decompress2(src, cap: int = 1 << 24) -> bytes:
+    """`fse_decompress2(src, &mut dst) -> Option<usize>` (lib.rs:215)."""
+    a = _buf(src)
+    lib = load()
+    dst = np.zeros(max(cap, 1), dtype=np.uint8)
+    n = C.c_size_t(0)
+    check(lib.fse_decompress2(_p(a), len(a), _p(dst), cap, C.byref(n)), "fse_decompress2")
+    return dst[: n.value].tobytes()
+
+
+def histogram_count(src) -> tuple[np.ndarray, int]:
+    """`Histogram::new(data)` (histogram.rs:18-66): (counts[256], table_len)."""
+    a = _buf(src)
+    lib = load()
+    counts = np.zeros(256, dtype=np.uint32)
+    tl = C.c_uint32(0)
+    check(lib.histogram_count(_p(a), len(a), _p(counts), C.byref(tl)), "histogram_count")
+    return counts, tl.value
+
+
+class BlockCodec:
+    """Batched device codec: 64 KiB blocks (configurable) over torch tensors.
+
+    compress(src) -> CompressedBlocks (slots, lengths, sidecar, status), all
+    resident on the device; decompress(cb) -> uint8 tensor.  Work is queued
+    on torch's current stream.
+    """
+
+    def __init__(self, block_size: int = 65536, table_log: int = 0, ckpt_interval: int = 512,
+                 device=None):
+        import torch
+
+        self.torch = torch
+        self.device = torch.device(device or "cuda")
+        self.block_size = block_size
+        self.table_log = table_log
+        self.ckpt_interval = ckpt_interval
+        self.max_table_log = max(11, table_log) if table_log else 11
+        self.lib = load()
+        self.slot_bytes = int(self.lib.fsehip_slot_bytes(block_size, self.max_table_log))
+        self.side_per_block = int(self.lib.fsehip_sidecar_per_block(block_size, ckpt_interval))
+
+    def params(self) -> Params:
+        return Params(self.block_size, self.table_log, self.ckpt_interval, self.max_table_log)
+
+    def _stream(self):
+        return C.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
+
+    def n_blocks(self, n_total: int) -> int:
+        return (n_total + self.block_size - 1) // self.block_size
+
+    def alloc(self, n_total: int) -> dict:
+        t = self.torch
+        nb = self.n_blocks(n_total)
+        return {
+            "n_total": n_total,
+            "out": t.empty(nb * self.slot_bytes, dtype=t.uint8, device=self.device),
+            "comp_len": t.zeros(nb, dtype=t.int32, device=self.device),
+            "payload_bits": t.zeros(nb, dtype=t.int32, device=self.device),
+            "sidecar": t.zeros(max(nb * self.side_per_block, 1), dtype=t.int64, device=self.device),
+            "status": t.zeros(nb, dtype=t.int32, device=self.device),
+        }
+
+    def compress_into(self, src, cb: dict) -> None:
+        p = self.params()
+        rc = self.lib.fsehip_compress_blocks(
+            C.byref(p), C.c_void_p(src.data_ptr()), cb["n_total"], C.c_void_p(cb["out"].data_ptr()),
+            self.slot_bytes, C.c_void_p(cb["comp_len"].data_ptr()),
+            C.c_void_p(cb["payload_bits"].data_ptr()),
+            C.c_void_p(cb["sidecar"].data_ptr()) if self.ckpt_interval else None,
+            C.c_void_p(cb["status"].data_ptr()), self._stream())
+        check(rc, "fsehip_compress_blocks")
+
+    def compress(self, src) -> dict:
+        cb = self.alloc(src.numel())
+        self.compress_into(src, cb)
+        return cb
+
+    def decompress_into(self, cb: dict, out, status, use_sidecar: bool = True) -> None:
+        p = self.params()
+        side = C.c_void_p(cb["sidecar"].data_ptr()) if (use_sidecar and self.ckpt_interval) else None
+        rc = self.lib.fsehip_decompress_blocks(
+            C.byref(p), C.c_void_p(cb["out"].data_ptr()), self.slot_bytes,
+            C.c_void_p(cb["comp_len"].data_ptr()), side, C.c_void_p(out.data_ptr()), cb["n_total"],
+            C.c_void_p(status.data_ptr()), self._stream())
+        check(rc, "fsehip_decompress_blocks")
+
+    def decompress(self, cb: dict, use_sidecar: bool = True):
+        t = self.torch
+        out = t.empty(cb["n_total"], dtype=t.uint8, device=self.device)
+        status = t.zeros(self.n_blocks(cb["n_total"]), dtype=t.int32, device=self.device)
+        self.decompress_into(cb, out, status, use_sidecar)
+        return out, status
+
+    def generate(self, kind: int, prob: float, seed: int, n_total: int):
+        t = self.torch
+        out = t.empty(n_total, dtype=t.uint8, device=self.device)
+        check(self.lib.fsehip_generate(kind, prob, seed, self.block_size, C.c_void_p(out.data_ptr()),
+                                       n_total, self._stream()), "fsehip_generate")
+        return out
+
+    def block_bytes(self, cb: dict, b: int) -> bytes:
+        """Compressed bytes of block b (host copy) -- for parity checks."""
+        ln = int(cb["comp_len"][b].item())
+        s = b * self.slot_bytes
+        return cb["out"][s: s + ln].cpu().numpy().tobytes()
+
+
+__all__ = ["BlockCodec", "FseError", "compress2", "compress2_log", "decompress2", "histogram_count"]

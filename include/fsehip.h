@@ -1,0 +1,119 @@
+/*
+ * fsehip.h -- C ABI of the MI355X-native FSE (tANS) entropy coder.
+ *
+ * Drop-in boundary for the hot path of Cognoscan/entropy_coders (a Rust
+ * crate).  Two layers:
+ *
+ *  (1) Reference-shaped entry points (host pointers, one block per call),
+ *      one per public function of the crate on this path.  They keep the
+ *      crate's argument meaning and its "append to dst" convention; Rust
+ *      panics / None / Err become negative status codes (fse_status.h).
+ *      Compute runs on the GPU; there is no CPU fallback.  These are what a
+ *      Rust FFI shim binds.
+ *
+ *  (2) Batched device entry points (fsehip_*): all pointers are device
+ *      pointers, calls are asynchronous on `stream` and report a status per
+ *      block.  This is the throughput path (bench.py, multi-GPU sharding).
+ *
+ * Every compressed block is byte-identical to the crate's fse_compress2
+ * output for the same input (lib.rs:146-183).
+ */
+#ifndef FSEHIP_H
+#define FSEHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "fse_status.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* fsehip_stream_t; /* hipStream_t; NULL = the null stream */
+
+/* ------------------------------------------------------------------------
+ * (1) Reference-shaped entry points
+ * ------------------------------------------------------------------------ */
+
+/* Replaces `pub fn fse_compress2(src: &[u8], dst: &mut Vec<u8>) -> usize`
+ * (lib.rs:146).  Appends header||payload at dst[*dst_len], advances
+ * *dst_len, and stores the Rust return value (payload bits incl. marker) in
+ * *payload_bits.  Errors: EMPTY, TOO_SHORT, ALL_ZERO_SYMBOL0 (reference
+ * panics), DST_TOO_SMALL (the reference grows its Vec), UNSUPPORTED. */
+int fse_compress2(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, size_t* dst_len,
+                  uint64_t* payload_bits);
+
+/* `Histogram::new(src).normalize(table_log)` followed by the fse_compress2
+ * body (histogram.rs:95 + lib.rs:149-182): the tableLog sweep entry point. */
+int fse_compress2_log(const uint8_t* src, size_t n, uint32_t table_log, uint8_t* dst, size_t dst_cap,
+                      size_t* dst_len, uint64_t* payload_bits);
+
+/* Replaces `pub fn fse_decompress2(src: &[u8], dst: &mut Vec<u8>)
+ * -> Option<usize>` (lib.rs:215).  Appends the decoded bytes at
+ * dst[*dst_len] and advances *dst_len.  None -> BAD_HEADER / NO_MARKER;
+ * the state-read panic -> TOO_SHORT; the never-terminating single-symbol
+ * case -> SINGLE_SYMBOL. */
+int fse_decompress2(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, size_t* dst_len);
+
+/* Replaces `Histogram::new(data)` (histogram.rs:18-66) -- the north star's
+ * `histogram::count`: counts[256], table_len = 1 + largest symbol. */
+int histogram_count(const uint8_t* src, size_t n, uint32_t counts[256], uint32_t* table_len);
+
+/* ------------------------------------------------------------------------
+ * (2) Batched device entry points
+ * ------------------------------------------------------------------------ */
+
+typedef struct {
+    uint32_t block_size;    /* bytes per block; multiple of 16 when >1 block; default 65536 */
+    uint32_t table_log;     /* 0 = NormHistogram::new (optimal); else Histogram::normalize(L) */
+    uint32_t ckpt_interval; /* pairs between decode checkpoints (power of two >= 8), 0 = none */
+    uint32_t max_table_log; /* upper bound on L used by the blocks (11 or 12); 0 = derive */
+} fsehip_params;
+
+/* Per-block output slot size (bytes) able to hold any block of block_size
+ * bytes at tableLog <= max_table_log, and sidecar entries per block. */
+uint64_t fsehip_slot_bytes(uint32_t block_size, uint32_t max_table_log);
+uint32_t fsehip_sidecar_per_block(uint32_t block_size, uint32_t ckpt_interval);
+
+/* Compress n_total bytes as ceil(n_total/block_size) independent blocks.
+ * Block b's bytes go to d_out + b*slot_bytes (comp_len[b] bytes, exactly
+ * fse_compress2's output); d_sidecar (optional) receives the decode
+ * checkpoints: entry = bitpos(32, payload-relative) | s0<<32 | s1<<48 for
+ * the decoder state before pair k*ckpt_interval. */
+int fsehip_compress_blocks(const fsehip_params* p, const uint8_t* d_src, uint64_t n_total, uint8_t* d_out,
+                           uint64_t slot_bytes, uint32_t* d_comp_len, uint32_t* d_payload_bits,
+                           uint64_t* d_sidecar, int32_t* d_status, fsehip_stream_t stream);
+
+/* Decompress blocks produced as above.  With d_sidecar the blocks decode in
+ * parallel segments; without it each block decodes serially (any valid
+ * fse_compress2 stream).  n_total (> 0) gives the raw length. */
+int fsehip_decompress_blocks(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
+                             const uint32_t* d_comp_len, const uint64_t* d_sidecar, uint8_t* d_out,
+                             uint64_t n_total, int32_t* d_status, fsehip_stream_t stream);
+
+/* Serial decode that also records the sidecar index (for streams produced
+ * elsewhere, e.g. by the CPU crate), so later decodes run in parallel. */
+int fsehip_build_sidecar(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
+                         const uint32_t* d_comp_len, uint8_t* d_out, uint64_t n_total, uint64_t* d_sidecar_out,
+                         int32_t* d_status, fsehip_stream_t stream);
+
+/* histogram::count per block: d_counts[b*256 + s], d_table_len[b]. */
+int fsehip_histogram_blocks(const uint8_t* d_src, uint64_t n_total, uint32_t block_size, uint32_t* d_counts,
+                            uint32_t* d_table_len, fsehip_stream_t stream);
+
+/* Synthetic input (bench/tests): kind 0 = LUT generator of
+ * benches/fse_benchmark.rs:5-20 with probability prob, 1 = geometric p=0.5,
+ * 2 = uniform 0..239; counter-based splitmix64 (see oracle fo_generate). */
+int fsehip_generate(int kind, double prob, uint64_t seed, uint32_t block_size, uint8_t* d_out,
+                    uint64_t n_total, fsehip_stream_t stream);
+
+/* Device count visible to this process (0 when HIP is unusable). */
+int fsehip_device_count(void);
+/* Library build identifier. */
+const char* fsehip_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
