@@ -36,7 +36,7 @@ def parse():
     ap.add_argument("--prob", type=float, default=0.155)
     ap.add_argument("--kind", type=int, default=0)
     ap.add_argument("--table-log", type=int, default=0)
-    ap.add_argument("--ckpt", type=int, default=512)
+    ap.add_argument("--ckpt", type=int, default=128)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     return ap.parse_args()

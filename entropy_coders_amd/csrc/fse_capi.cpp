@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#include <stdlib.h>
+
 #include <algorithm>
 #include <mutex>
 #include <vector>
@@ -19,6 +21,13 @@ namespace {
 constexpr uint32_t kDefaultBlock = 65536;
 
 uint64_t round_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+
+// Tuning / ablation knobs (not part of the ABI): FSEHIP_ENC_LANES=32|64,
+// FSEHIP_DEBUG bit mask (see fse_kernels.h).
+uint32_t env_u32(const char* name, uint32_t dflt) {
+    const char* v = getenv(name);
+    return v && *v ? (uint32_t)strtoul(v, nullptr, 0) : dflt;
+}
 
 bool device_ok() {
     int n = 0;
@@ -156,6 +165,8 @@ int fsehip_compress_blocks(const fsehip_params* p, const uint8_t* d_src, uint64_
     P.payload_bits = d_payload_bits;
     P.sidecar = P.ckpt_interval ? d_sidecar : nullptr;
     P.status = d_status;
+    P.lanes = env_u32("FSEHIP_ENC_LANES", 64) == 32 ? 32 : 64;
+    P.debug = env_u32("FSEHIP_DEBUG", 0);
     hipError_t e = fsehip::launch_encode(P, lmax, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? FSE_OK : FSE_ERR_HIP;
 }
@@ -188,6 +199,7 @@ static int decompress_impl(const fsehip_params* p, const uint8_t* d_in, uint64_t
     P.status = d_status;
     P.out_len = d_out_len;
     P.sidecar_out = d_sidecar_out;
+    P.debug = env_u32("FSEHIP_DEBUG", 0) >> 4;
     // the decoder reads L from each header; size its tables for the bound
     uint32_t lmax = p->max_table_log ? p->max_table_log : 12;
     hipError_t e = fsehip::launch_decode(P, lmax, static_cast<hipStream_t>(stream));

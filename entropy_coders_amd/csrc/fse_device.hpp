@@ -23,6 +23,14 @@ __device__ __forceinline__ uint32_t ilog2u(uint32_t x) { return 31u - (uint32_t)
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 __device__ __forceinline__ uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
 
+// Synchronise the lanes of one wave around LDS traffic.  A wave's LDS
+// operations execute in order, so only compiler reordering must be stopped;
+// this lets the wave-level builders below run inside multi-wave workgroups.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
 // Inclusive prefix sum across the wave (6 DPP-able shuffle steps).
 __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
 #pragma unroll
@@ -72,13 +80,30 @@ __device__ inline uint32_t wave_histogram(const uint8_t* __restrict__ src, uint3
                                           uint32_t* h4 /*LDS [4][256]*/, uint32_t* counts /*LDS[256]*/) {
     const uint32_t lane = lane_id();
     for (uint32_t i = lane; i < 1024; i += WAVE) h4[i] = 0;
-    __syncthreads();
+    wave_sync();
     uint32_t* mine = h4 + (lane & 3u) * 256u;
     uint32_t done = 0;
     if ((reinterpret_cast<uintptr_t>(src) & 15u) == 0) {
+        // 8 x 16-byte loads in flight per lane, then count them
+        constexpr uint32_t U = 8;
         const uint32_t nvec = n >> 4;
         const uint4* v4 = reinterpret_cast<const uint4*>(src);
-        for (uint32_t v = lane; v < nvec; v += WAVE) {
+        uint32_t v = 0;
+        for (; v + U * WAVE <= nvec; v += U * WAVE) {
+            uint4 d[U];
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) d[u] = v4[v + u * WAVE + lane];
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) {
+                const uint32_t w[4] = {d[u].x, d[u].y, d[u].z, d[u].w};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) atomicAdd(&mine[(w[k] >> (8 * b)) & 0xFFu], 1u);
+                }
+            }
+        }
+        for (v += lane; v < nvec; v += WAVE) {
             uint4 d = v4[v];
             uint32_t w[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
@@ -90,7 +115,7 @@ __device__ inline uint32_t wave_histogram(const uint8_t* __restrict__ src, uint3
         done = nvec << 4;
     }
     for (uint32_t i = done + lane; i < n; i += WAVE) atomicAdd(&mine[src[i]], 1u);
-    __syncthreads();
+    wave_sync();
     uint32_t tl = 0;
     for (uint32_t s = lane; s < 256; s += WAVE) {
         uint32_t c = h4[s] + h4[256 + s] + h4[512 + s] + h4[768 + s];
@@ -98,7 +123,7 @@ __device__ inline uint32_t wave_histogram(const uint8_t* __restrict__ src, uint3
         if (c) tl = max(tl, s + 1u);
     }
     tl = wave_max(tl);
-    __syncthreads();
+    wave_sync();
     return tl == 0 ? 1u : tl;
 }
 
@@ -227,24 +252,24 @@ __device__ inline int wave_normalize(const uint32_t* counts, uint32_t size, uint
     *used_slow = 0;
     if (single) {  // t == size returns immediately (113-120); other counts are 0
         if (lane == 0) norm[single - 1u] = (int32_t)(1u << L);
-        __syncthreads();
+        wave_sync();
         *L_out = L;
         return FSE_OK;
     }
     const int32_t to_distribute = (int32_t)(1u << L) - (int32_t)sum;
     const int32_t largest_prob = (int32_t)(best >> 8);
     const uint32_t largest = best ? 255u - (best & 255u) : 0u;
-    __syncthreads();
+    wave_sync();
     int rc = FSE_OK;
     if (to_distribute != 0 && -to_distribute >= (largest_prob >> 1)) {
         *used_slow = 1;
         if (lane == 0) scratch[0] = normalize_slow_lane(counts, size, tl, L, norm);
-        __syncthreads();
+        wave_sync();
         rc = scratch[0];
     } else {
         if (lane == 0) norm[largest] += to_distribute;
     }
-    __syncthreads();
+    wave_sync();
     *L_out = L;
     return rc;
 }
@@ -316,15 +341,16 @@ __device__ inline int header_write_lane(const int32_t* norm, uint32_t L, uint32_
 // ---------------------------------------------------------------------------
 struct FwdReader {
     const uint8_t* buf;
-    uint32_t total;  // bits
+    uint32_t total;  // bits (8 * slice length, stream_reader.rs:16)
     uint32_t pos;
+    uint32_t avail;  // bytes actually readable at buf (<= total / 8)
     __device__ bool peek(uint32_t nb, uint32_t* v) const {
         if (pos + nb > total) return false;
         uint32_t b = pos >> 3, sh = pos & 7u;
         uint64_t w = 0;
         uint32_t nbytes = (sh + nb + 7u) >> 3;
         for (uint32_t i = 0; i < nbytes; ++i)
-            if (b + i < (total >> 3)) w |= (uint64_t)buf[b + i] << (8u * i);
+            if (b + i < avail) w |= (uint64_t)buf[b + i] << (8u * i);
         *v = (uint32_t)((w >> sh) & ((1ull << nb) - 1ull));
         return true;
     }
@@ -335,10 +361,10 @@ struct FwdReader {
     }
 };
 
-__device__ inline int header_read_lane(const uint8_t* src, uint32_t n, int32_t* norm, uint32_t* L_out,
-                                       uint32_t* tl_out) {
+__device__ inline int header_read_lane(const uint8_t* src, uint32_t n, uint32_t avail, int32_t* norm,
+                                       uint32_t* L_out, uint32_t* tl_out) {
     if (n == 0) return FSE_ERR_EMPTY;
-    FwdReader r{src, n * 8u, 0};
+    FwdReader r{src, n * 8u, 0, min(avail, n)};
     uint32_t v;
     if (!r.peek(4, &v)) return FSE_ERR_BAD_HEADER;
     r.advance(4);
@@ -441,7 +467,7 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
     const int32_t ht = (int32_t)size - 1 - (int32_t)total_neg;
     for (uint32_t i = lane; i < size; i += WAVE) { occ_sym[i] = 0; sym_at[i] = 0; }
     for (uint32_t s = lane; s < 256; s += WAVE) cnt[s] = 0;
-    __syncthreads();
+    wave_sync();
     {
         uint32_t c = ex_c, p = ex_p, ng = ex_n;
 #pragma unroll
@@ -455,7 +481,7 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
             ng += neg[k];
         }
     }
-    __syncthreads();
+    wave_sync();
     // forward max-fill: occ_sym[j] = owner of positive occurrence j
     {
         uint32_t carry = 0;
@@ -467,7 +493,7 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
             carry = __shfl(f, 63, 64);
         }
     }
-    __syncthreads();
+    wave_sync();
     // spread: j-th valid multiplier -> position
     const uint32_t step = (size >> 3) * 5u + 3u;  // table_step: size*5/8+3 (fse.rs:67-70)
     {
@@ -484,7 +510,7 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
         }
         if (j0 != total_pos) return FSE_ERR_BAD_TABLE;  // position != 0 assert
     }
-    __syncthreads();
+    wave_sync();
     // occurrence ranks in ascending position order
     for (uint32_t base = 0; base < size; base += WAVE) {
         uint32_t i = base + lane;
@@ -494,11 +520,11 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
         uint64_t peers = match_u8(s, active);
         uint32_t before = act ? cnt[s] : 0u;
         uint32_t r = before + (uint32_t)__popcll(peers & lanemask_lt());
-        __syncthreads();
+        wave_sync();
         bool leader = act && ((peers & lanemask_lt()) == 0);
         if (leader) cnt[s] = before + (uint32_t)__popcll(peers);
         if (act) visit(i, s, r);
-        __syncthreads();
+        wave_sync();
     }
     return FSE_OK;
 }

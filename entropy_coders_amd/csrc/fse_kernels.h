@@ -20,6 +20,8 @@ struct EncParams {
     uint32_t* payload_bits;
     uint64_t* sidecar;
     int32_t* status;
+    uint32_t lanes;  // encoder lanes per block (32 or 64; 0 = default)
+    uint32_t debug;  // ablation: bit0 = tables only, bit1 = no emit pass
 };
 
 struct DecParams {
@@ -37,6 +39,7 @@ struct DecParams {
     int32_t* status;
     uint32_t* out_len;
     uint64_t* sidecar_out;  // serial mode: record checkpoints here
+    uint32_t debug;         // ablation: bit0 = header + table only
 };
 
 struct GenParams {

@@ -32,29 +32,32 @@ __device__ __forceinline__ uint4 load_chunk(const uint8_t* blk, uint32_t n, uint
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-// Encoder state step (Encoder::encode_raw, fse.rs:227-239).
+// Encoder tables in LDS: stateTable as bytes and the symbol transforms
+// {deltaNbBits, byte offset of stateTable[deltaFindState]} (fse.rs:165-188),
+// so one state step is add, shift, shift-add, ds_read_u16.
 struct EncTab {
-    const uint16_t* st;
-    const uint2* tt;  // {deltaNbBits, deltaFindState}
+    const uint8_t* st;  // stateTable, u16 entries (fse.rs:157-162)
+    const uint2* tt;    // {deltaNbBits, 2 * deltaFindState}
 };
 
 // Bit emitter into a 32-bit-word view of the output slot.  Bits are
-// appended LSB-first (writer.rs:140-180); the first word is partial when the
-// lane's offset is not word aligned and is handed to the merge step.
+// appended LSB-first (writer.rs:140-180); every completed word is stored,
+// including the lane's first word, whose low bits belong to the previous
+// lane: the merge step later rewrites each boundary word with the OR of both
+// lanes' bits.
 struct Emit {
     uint64_t acc;
     uint32_t nacc;
     uint32_t word;
+    uint32_t w0;        // first word index of the lane
+    uint32_t head_val;  // lane's bits of word w0 once it was stored
     uint32_t* gw;
-    bool head;
-    uint32_t head_word, head_val;
     __device__ __forceinline__ void start(uint32_t* g, uint32_t off) {
         gw = g;
         acc = 0;
         nacc = off & 31u;
         word = off >> 5;
-        head = nacc != 0;
-        head_word = 0xFFFFFFFFu;
+        w0 = word;
         head_val = 0;
     }
     __device__ __forceinline__ void put(uint32_t v, uint32_t nb) {
@@ -62,26 +65,20 @@ struct Emit {
         nacc += nb;
     }
     __device__ __forceinline__ void flush() {
-        if (nacc >= 32) {
-            uint32_t val = (uint32_t)acc;
-            if (head) {
-                head = false;
-                head_word = word;
-                head_val = val;
-            } else {
-                gw[word] = val;
-            }
-            word++;
-            acc >>= 32;
-            nacc -= 32;
-        }
+        const bool f = nacc >= 32u;
+        const uint32_t val = (uint32_t)acc;
+        if (f) gw[word] = val;
+        head_val = (f && word == w0) ? val : head_val;
+        acc = f ? (acc >> 32) : acc;
+        nacc -= f ? 32u : 0u;
+        word += f ? 1u : 0u;
     }
     __device__ __forceinline__ uint32_t pos() const { return word * 32u + nacc; }
 };
 
 struct Ckpt {
     uint64_t* base;  // this block's sidecar entries, or nullptr
-    uint32_t mask;   // interval - 1 (interval is a power of two)
+    uint32_t mask;   // interval - 1 (interval is a power of two, >= 8)
     uint32_t shift;  // log2(interval)
     uint32_t hdr_bits;
     uint32_t L;
@@ -89,47 +86,93 @@ struct Ckpt {
 
 enum { PASS_SPEC = 0, PASS_COUNT = 1, PASS_EMIT = 2 };
 
-template <int MODE>
-__device__ __forceinline__ void enc_sym(uint32_t& x, uint32_t s, const EncTab& T, uint32_t& bits, Emit& em) {
+struct EncState {
+    uint32_t x0, x1, bits;
+};
+
+// Encoder::encode_raw (fse.rs:227-239): returns nb, updates x.
+__device__ __forceinline__ uint32_t enc_step(uint32_t& x, uint32_t s, const EncTab& T) {
     const uint2 t = T.tt[s];
     const uint32_t nb = (t.x + x) >> 16;
-    if (MODE == PASS_COUNT) bits += nb;
-    if (MODE == PASS_EMIT) em.put(x & ((1u << nb) - 1u), nb);
-    x = T.st[(int32_t)(x >> nb) + (int32_t)t.y];
+    x = *reinterpret_cast<const uint16_t*>(T.st + ((x >> nb) << 1) + (int32_t)t.y);
+    return nb;
 }
 
-// Encode pairs pb-1 down to pa (lib.rs:167-176: E1 then E0 per pair).
-template <int MODE>
-__device__ void enc_range(const uint8_t* __restrict__ blk, uint32_t n, uint32_t pa, uint32_t pb, uint32_t& x0,
-                          uint32_t& x1, const EncTab& T, uint32_t& bits, Emit& em, const Ckpt& ck) {
-    if (pb <= pa) return;
-    const int32_t c_hi = (int32_t)((pb - 1u) >> 3), c_lo = (int32_t)(pa >> 3);
-    uint4 cur = load_chunk(blk, n, (uint32_t)c_hi);
-    for (int32_t c = c_hi; c >= c_lo; --c) {
-        uint4 nxt = (c > c_lo) ? load_chunk(blk, n, (uint32_t)(c - 1)) : make_uint4(0, 0, 0, 0);
-        const uint32_t w[4] = {cur.x, cur.y, cur.z, cur.w};
+// One 16-byte chunk = pairs c8+7 .. c8 (lib.rs:167-176: E1 then E0 per
+// pair).  FULL chunks need no guard; only the topmost chunk of the topmost
+// lane can extend past the last main-loop pair pb.
+template <int MODE, bool FULL>
+__device__ __forceinline__ void enc_chunk(const uint4& q, uint32_t c8, uint32_t pb, uint32_t& x0, uint32_t& x1,
+                                          const EncTab& T, uint32_t& bits, Emit& em) {
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-        for (int j = 7; j >= 0; --j) {
-            const uint32_t p = (uint32_t)c * 8u + (uint32_t)j;
-            if (p < pb && p >= pa) {
-                const uint32_t sh = 16u * (uint32_t)(j & 1);
-                const uint32_t s0 = (w[j >> 1] >> sh) & 0xFFu;
-                const uint32_t s1 = (w[j >> 1] >> (sh + 8u)) & 0xFFu;
-                enc_sym<MODE>(x1, s1, T, bits, em);
-                enc_sym<MODE>(x0, s0, T, bits, em);
-                if (MODE == PASS_EMIT) {
-                    em.flush();
-                    if (ck.base && (p & ck.mask) == 0u) {
-                        const uint64_t e = (uint64_t)(em.pos() - ck.hdr_bits) |
-                                           ((uint64_t)(x0 - (1u << ck.L)) << 32) |
-                                           ((uint64_t)(x1 - (1u << ck.L)) << 48);
-                        ck.base[p >> ck.shift] = e;
-                    }
-                }
-            }
+    for (int j = 7; j >= 0; --j) {
+        if (!FULL && c8 + (uint32_t)j >= pb) continue;
+        const uint32_t sh = 16u * (uint32_t)(j & 1);
+        const uint32_t s0 = (w[j >> 1] >> sh) & 0xFFu;
+        const uint32_t s1 = (w[j >> 1] >> (sh + 8u)) & 0xFFu;
+        const uint32_t v1 = x1, v0 = x0;
+        const uint32_t nb1 = enc_step(x1, s1, T);
+        const uint32_t nb0 = enc_step(x0, s0, T);
+        if (MODE == PASS_COUNT) bits += nb1 + nb0;
+        if (MODE == PASS_EMIT) {
+            const uint32_t pairbits = (v1 & ((1u << nb1) - 1u)) | ((v0 & ((1u << nb0) - 1u)) << nb1);
+            em.put(pairbits, nb1 + nb0);
+            em.flush();
         }
-        cur = nxt;
     }
+}
+
+// Sidecar entry for the decoder state before pair p (= encoder state after
+// encoding pair p): bit position (payload-relative) and both states.
+__device__ __forceinline__ void ckpt_record(const Ckpt& ck, uint32_t p, uint32_t pos, uint32_t x0, uint32_t x1) {
+    ck.base[p >> ck.shift] = (uint64_t)(pos - ck.hdr_bits) | ((uint64_t)(x0 - (1u << ck.L)) << 32) |
+                             ((uint64_t)(x1 - (1u << ck.L)) << 48);
+}
+
+// Encode pairs pb-1 down to pa.  Source chunks (16 B = 8 pairs) stream
+// through four fixed registers, each reloaded right after it is consumed,
+// so three loads stay in flight and no register copy forces an early
+// s_waitcnt.  Loads are unconditional (the index is clamped to the
+// segment); the partial topmost chunk is peeled and loaded byte-wise.
+template <int MODE>
+__device__ __forceinline__ EncState enc_range(const uint8_t* __restrict__ blk, uint32_t n, uint32_t pa, uint32_t pb,
+                                              EncState st, const EncTab& T, Emit& em, const Ckpt& ck) {
+    uint32_t x0 = st.x0, x1 = st.x1, bits = st.bits;
+    if (pb <= pa) return st;
+    const uint4* v = reinterpret_cast<const uint4*>(blk);
+    int32_t c_hi = (int32_t)((pb - 1u) >> 3);
+    const int32_t c_lo = (int32_t)(pa >> 3);
+    if (pb & 7u) {  // partial topmost chunk
+        const uint4 q = load_chunk(blk, n, (uint32_t)c_hi);
+        enc_chunk<MODE, false>(q, (uint32_t)c_hi * 8u, pb, x0, x1, T, bits, em);
+        if (MODE == PASS_EMIT && ck.base && (((uint32_t)c_hi * 8u) & ck.mask) == 0u)
+            ckpt_record(ck, (uint32_t)c_hi * 8u, em.pos(), x0, x1);
+        c_hi -= 1;
+    }
+    if (c_hi < c_lo) return EncState{x0, x1, bits};
+    auto ld = [&](int32_t c) { return v[c < c_lo ? c_lo : c]; };
+    uint4 q0 = ld(c_hi), q1 = ld(c_hi - 1), q2 = ld(c_hi - 2), q3 = ld(c_hi - 3);
+    auto body = [&](const uint4& q, int32_t c) {
+        enc_chunk<MODE, true>(q, (uint32_t)c * 8u, pb, x0, x1, T, bits, em);
+        if (MODE == PASS_EMIT && ck.base && (((uint32_t)c * 8u) & ck.mask) == 0u)
+            ckpt_record(ck, (uint32_t)c * 8u, em.pos(), x0, x1);
+    };
+    for (int32_t c = c_hi;; c -= 4) {
+        body(q0, c);
+        if (c - 1 < c_lo) break;
+        q0 = ld(c - 4);
+        body(q1, c - 1);
+        if (c - 2 < c_lo) break;
+        q1 = ld(c - 5);
+        body(q2, c - 2);
+        if (c - 3 < c_lo) break;
+        q2 = ld(c - 6);
+        body(q3, c - 3);
+        if (c - 4 < c_lo) break;
+        q3 = ld(c - 7);
+    }
+    return EncState{x0, x1, bits};
 }
 
 // Encoder::new_first_symbol, fse.rs:210-218
@@ -137,7 +180,30 @@ __device__ __forceinline__ uint32_t enc_init(const EncTab& T, uint32_t s) {
     const uint2 t = T.tt[s];
     const uint32_t bo = (t.x + (1u << 15)) >> 16;
     const uint32_t v = (bo << 16) - t.x;
-    return T.st[(int32_t)(v >> bo) + (int32_t)t.y];
+    return *reinterpret_cast<const uint16_t*>(T.st + ((v >> bo) << 1) + (int32_t)t.y);
+}
+
+// Exact state of the topmost lane before the main loop: both encoders seeded
+// with the last symbols, plus the odd-length extra step (lib.rs:153-165).
+template <int MODE>
+__device__ __forceinline__ EncState top_start(const uint8_t* blk, uint32_t n, const EncTab& tab, Emit& em) {
+    EncState e;
+    e.bits = 0;
+    if (n & 1u) {  // lib.rs:155-160
+        e.x0 = enc_init(tab, blk[n - 1u]);
+        e.x1 = enc_init(tab, blk[n - 2u]);
+        const uint32_t v0 = e.x0;
+        const uint32_t nb = enc_step(e.x0, blk[n - 3u], tab);
+        if (MODE == PASS_COUNT) e.bits = nb;
+        if (MODE == PASS_EMIT) {
+            em.put(v0 & ((1u << nb) - 1u), nb);
+            em.flush();
+        }
+    } else {  // lib.rs:161-165
+        e.x0 = enc_init(tab, blk[n - 2u]);
+        e.x1 = enc_init(tab, blk[n - 1u]);
+    }
+    return e;
 }
 
 // ------------------------------------------------------------------------
@@ -218,11 +284,11 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
                         t.x = ((L + 1u) << 16) - (1u << L);
                     } else if (x == -1 || x == 1) {
                         t.x = (L << 16) - (1u << L);
-                        t.y = (uint32_t)(tot - 1);
+                        t.y = (uint32_t)(2 * (tot - 1));
                     } else {
                         const uint32_t mb = L - ilog2u((uint32_t)(x - 1));
                         t.x = (mb << 16) - ((uint32_t)x << mb);
-                        t.y = (uint32_t)(tot - x);
+                        t.y = (uint32_t)(2 * (tot - x));
                     }
                 }
                 sm.tt[b][s] = t;
@@ -241,16 +307,17 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
         __syncthreads();
     }
 
+    if (P.debug & 1u) return;  // ablation: statistics + tables only
     // ---- phase 2: T lanes per block
-    const int b = (int)(lane / T);
-    const uint32_t k = lane % T;
+    const int b = BPW == 1 ? 0 : (int)(lane / T);
+    const uint32_t k = BPW == 1 ? lane : lane % T;
     const uint64_t gb = (uint64_t)blockIdx.x * BPW + b;
     const bool live = sm.info_status[b] == FSE_OK;
     const uint64_t boff = gb * P.block_size;
     const uint32_t n = live ? (uint32_t)min((uint64_t)P.block_size, P.n_total - boff) : 0u;
     const uint8_t* blk = P.src + boff;
     const uint32_t L = sm.info_L[b];
-    const EncTab tab{sm.st[b], sm.tt[b]};
+    const EncTab tab{reinterpret_cast<const uint8_t*>(sm.st[b]), sm.tt[b]};
     const uint32_t Pm = live ? ((n & 1u) ? (n - 3u) / 2u : n / 2u - 1u) : 0u;
     uint32_t S = (Pm + T - 1u) / T;
     S = max(8u, (S + 7u) & ~7u);
@@ -260,63 +327,30 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     Emit em;
     em.start(nullptr, 0);
     Ckpt ck{nullptr, 0, 0, 0, L};
-    uint32_t bits = 0;
 
     // exact start of the top lane: init states (+ odd-length extra step)
-    auto top_start = [&](uint32_t& x0, uint32_t& x1, uint32_t& bts, Emit& e, bool emit, bool count) {
-        if (n & 1u) {  // lib.rs:155-160
-            x0 = enc_init(tab, blk[n - 1u]);
-            x1 = enc_init(tab, blk[n - 2u]);
-            const uint32_t s = blk[n - 3u];
-            const uint2 t = tab.tt[s];
-            const uint32_t nb = (t.x + x0) >> 16;
-            if (count) bts += nb;
-            if (emit) {
-                e.put(x0 & ((1u << nb) - 1u), nb);
-                e.flush();
-            }
-            x0 = tab.st[(int32_t)(x0 >> nb) + (int32_t)t.y];
-        } else {  // lib.rs:161-165
-            x0 = enc_init(tab, blk[n - 2u]);
-            x1 = enc_init(tab, blk[n - 1u]);
-        }
-    };
-
     // spec pass: lanes 1..ktop (the top lane runs exactly)
-    uint32_t x0 = 0, x1 = 0;
     if (act && k >= 1) {
-        if (k == ktop) {
-            top_start(x0, x1, bits, em, false, false);
-        } else {
-            x0 = x1 = 1u << L;
-        }
-        enc_range<PASS_SPEC>(blk, n, pa, pb, x0, x1, tab, bits, em, ck);
-        sm.specF[b][k] = x0 | (x1 << 16);
+        EncState e0 = (k == ktop) ? top_start<PASS_SPEC>(blk, n, tab, em) : EncState{1u << L, 1u << L, 0u};
+        e0 = enc_range<PASS_SPEC>(blk, n, pa, pb, e0, tab, em, ck);
+        sm.specF[b][k] = e0.x0 | (e0.x1 << 16);
     }
     __syncthreads();
 
-    // count pass from the neighbour's spec end state
-    uint32_t start = 0;
-    auto count_pass = [&](uint32_t st0) {
-        uint32_t y0, y1, bt = 0;
-        if (k == ktop) {
-            top_start(y0, y1, bt, em, false, true);
-        } else {
-            y0 = st0 & 0xFFFFu;
-            y1 = st0 >> 16;
-        }
-        enc_range<PASS_COUNT>(blk, n, pa, pb, y0, y1, tab, bt, em, ck);
-        if (k == 0) bt += 2u * L + 1u;  // finals + marker (lib.rs:178-181)
-        sm.cntF[b][k] = y0 | (y1 << 16);
-        return bt;
-    };
-    if (act) {
-        start = (k < ktop) ? sm.specF[b][k + 1] : 0u;
-        bits = count_pass(start);
-    }
-    // verify: a lane's start must equal its neighbour's exact end state.
-    // Iterates to the unique fixed point (the top lane is exact).
+    // count pass from the neighbour's spec end state, then verify: a lane's
+    // start must equal its neighbour's exact end state.  Iterating to the
+    // unique fixed point (the top lane is exact) makes every lane exact.
+    uint32_t start = (act && k < ktop) ? sm.specF[b][k + 1] : 0u;
+    uint32_t bits = 0;
+    bool need = act;
     for (;;) {
+        if (need) {
+            EncState e0 = (k == ktop) ? top_start<PASS_COUNT>(blk, n, tab, em)
+                                      : EncState{start & 0xFFFFu, start >> 16, 0u};
+            e0 = enc_range<PASS_COUNT>(blk, n, pa, pb, e0, tab, em, ck);
+            bits = e0.bits + (k == 0 ? 2u * L + 1u : 0u);  // finals + marker (lib.rs:178-181)
+            sm.cntF[b][k] = e0.x0 | (e0.x1 << 16);
+        }
         __syncthreads();
         bool bad = false;
         uint32_t nbF = 0;
@@ -326,10 +360,8 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
         }
         __syncthreads();
         if (__ballot(bad) == 0) break;
-        if (bad) {
-            start = nbF;
-            bits = count_pass(start);
-        }
+        if (bad) start = nbF;
+        need = bad;
     }
 
     // offsets: lane k writes after every lane j > k (stack order)
@@ -344,7 +376,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     }
     const uint32_t total_bits = hdr_bits + __shfl(suffix, 0, T);
     const uint32_t off = hdr_bits + suffix - mybits;
-    const bool fits = (uint64_t)total_bits <= P.slot_bytes * 8ull;
+    const bool fits = (uint64_t)total_bits <= P.slot_bytes * 8ull && !(P.debug & 2u);
     uint32_t* gw = reinterpret_cast<uint32_t*>(P.out + gb * P.slot_bytes);
 
     // emit pass
@@ -360,18 +392,18 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
             ck.shift = 31u - __clz(P.ckpt_interval);
             ck.hdr_bits = hdr_bits;
         }
-        uint32_t y0, y1, bt = 0;
+        EncState e0;
         if (k == ktop) {
-            top_start(y0, y1, bt, em, true, false);
+            e0 = top_start<PASS_EMIT>(blk, n, tab, em);
             if (ck.base && (Pm & ck.mask) == 0u) {  // checkpoint "before pair Pm"
-                ck.base[Pm >> ck.shift] = (uint64_t)(em.pos() - hdr_bits) | ((uint64_t)(y0 - (1u << L)) << 32) |
-                                          ((uint64_t)(y1 - (1u << L)) << 48);
+                ck.base[Pm >> ck.shift] = (uint64_t)(em.pos() - hdr_bits) | ((uint64_t)(e0.x0 - (1u << L)) << 32) |
+                                          ((uint64_t)(e0.x1 - (1u << L)) << 48);
             }
         } else {
-            y0 = start & 0xFFFFu;
-            y1 = start >> 16;
+            e0 = EncState{start & 0xFFFFu, start >> 16, 0u};
         }
-        enc_range<PASS_EMIT>(blk, n, pa, pb, y0, y1, tab, bt, em, ck);
+        e0 = enc_range<PASS_EMIT>(blk, n, pa, pb, e0, tab, em, ck);
+        const uint32_t y0 = e0.x0, y1 = e0.x1;
         if (k == 0) {  // Encoder::finish x2 + marker (lib.rs:178-181)
             const uint32_t m = (1u << L) - 1u;
             em.put(y1 & m, L);
@@ -383,11 +415,11 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
         }
         // boundary words -> merge list (entry order = stream order)
         const uint32_t slot = 2u * (T - k);
-        if (!em.head) {
-            sm.mword[b][slot] = em.head_word;
+        if ((off & 31u) != 0u && em.word > em.w0) {  // first word stored with the low bits empty
+            sm.mword[b][slot] = em.w0;
             sm.mval[b][slot] = em.head_val;
         }
-        if (em.nacc) {
+        if (em.nacc) {  // last word never stored
             sm.mword[b][slot + 1] = em.word;
             sm.mval[b][slot + 1] = (uint32_t)em.acc;
         }
@@ -405,6 +437,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
             sm.mval[b][0] = v;
         }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stores above land before the merge rewrites
     __syncthreads();
     // merge: each run of equal word indices is OR-ed by its first entry
     if (live && fits) {
@@ -445,21 +478,22 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
 // ------------------------------------------------------------------------
 // Decode
 // ------------------------------------------------------------------------
-// Backward bit reader over the block's 32-bit words (BitStackReader
-// semantics, stack_reader.rs:17-215): `pos` = bits remaining above the
-// block start; buf holds stream bits [base, base+64).
-struct BitReader {
-    const uint32_t* words;
+// Backward bit readers (BitStackReader semantics, stack_reader.rs:17-215):
+// `pos` = bits remaining above the block start, buf holds stream bits
+// [base, base+64) of the block; refills pull the next lower 32-bit word.
+// LdsReader reads the block staged in LDS; GlobalReader reads global memory
+// directly (blocks whose payload does not fit the LDS stage).
+struct LdsReader {
+    const uint32_t* w;
     uint64_t buf;
     int32_t base;
     int32_t pos;
-    __device__ __forceinline__ void init(const uint32_t* w, int32_t p) {
-        words = w;
+    __device__ __forceinline__ void init(const uint32_t* words, int32_t p) {
+        w = words;
         pos = p;
-        int32_t top = (p + 31) & ~31;
-        base = top - 64;
+        base = ((p + 31) & ~31) - 64;
         if (base < 0) base = 0;
-        buf = (uint64_t)words[base >> 5] | ((uint64_t)words[(base >> 5) + 1] << 32);
+        buf = (uint64_t)w[base >> 5] | ((uint64_t)w[(base >> 5) + 1] << 32);
     }
     __device__ __forceinline__ uint32_t pop(uint32_t nb) {
         pos -= (int32_t)nb;
@@ -468,185 +502,225 @@ struct BitReader {
     __device__ __forceinline__ void refill() {
         if (pos - base < 32 && base > 0) {
             base -= 32;
-            buf = (buf << 32) | (uint64_t)words[base >> 5];
+            buf = (buf << 32) | (uint64_t)w[base >> 5];
         }
     }
 };
-
-template <int LMAX>
-struct DecSmem {
-    static constexpr uint32_t SIZE = 1u << LMAX;
-    // dt[i] = new_state | symbol << 16 | nb << 24; the spread scratch lives
-    // in the top half of the same array (see wave_build_spread call).
-    uint32_t dt[SIZE];
-    int32_t norm[256];
-    uint16_t cumul[256];
-    uint32_t cnt[256];
-    int scratch[4];
-};
+using GlobalReader = LdsReader;  // same code, words in global memory
 
 __device__ __forceinline__ void store_byte(uint8_t* out, uint32_t i, uint32_t lim, uint32_t v) {
     if (i < lim) out[i] = (uint8_t)v;
 }
 
-template <int LMAX>
-__global__ __launch_bounds__(64) void decode_blocks_kernel(DecParams P) {
-    __shared__ DecSmem<LMAX> sm;
-    const uint32_t lane = lane_id();
+// Decode main-loop pairs [p0, p1) of one segment without read checks (the
+// sidecar guarantees the bits), 8 pairs per 16-byte store; when `last`,
+// finish with the reference termination in container mode (the oracle's
+// decompress2_impl; lib.rs:227-244).  Returns a status.
+template <class RD>
+__device__ __forceinline__ int32_t decode_segment(RD& br, uint32_t s0, uint32_t s1, uint32_t p0, uint32_t p1,
+                                                  bool last, uint32_t n, uint32_t Pm, uint8_t* __restrict__ out,
+                                                  const uint32_t* dt, uint32_t smask, int32_t hdr_bits) {
+    uint32_t p = p0;
+    for (; p + 8u <= p1; p += 8u) {
+        uint32_t w[4];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint32_t e0 = dt[s0 & smask], e1 = dt[s1 & smask];
+            const uint32_t v0 = br.pop(e0 >> 24);
+            const uint32_t v1 = br.pop(e1 >> 24);
+            s0 = ((e0 & 0xFFFFu) + v0) & 0xFFFFu;
+            s1 = ((e1 & 0xFFFFu) + v1) & 0xFFFFu;
+            const uint32_t pr = ((e0 >> 16) & 0xFFu) | ((e1 >> 8) & 0xFF00u);
+            if (j & 1) w[j >> 1] |= pr << 16; else w[j >> 1] = pr;
+            br.refill();
+        }
+        *reinterpret_cast<uint4*>(out + 2u * p) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    for (; p < p1; ++p) {
+        const uint32_t e0 = dt[s0 & smask], e1 = dt[s1 & smask];
+        const uint32_t v0 = br.pop(e0 >> 24);
+        const uint32_t v1 = br.pop(e1 >> 24);
+        s0 = ((e0 & 0xFFFFu) + v0) & 0xFFFFu;
+        s1 = ((e1 & 0xFFFFu) + v1) & 0xFFFFu;
+        out[2u * p] = (uint8_t)(e0 >> 16);
+        out[2u * p + 1u] = (uint8_t)(e1 >> 16);
+        br.refill();
+    }
+    if (!last) return FSE_OK;
+    uint32_t o = 2u * Pm;
+    for (;;) {
+        if (o + 2u == n) {
+            out[o++] = (uint8_t)(dt[s0 & smask] >> 16);
+            out[o++] = (uint8_t)(dt[s1 & smask] >> 16);
+            break;
+        }
+        if (o + 1u == n) {
+            out[o++] = (uint8_t)(dt[s0 & smask] >> 16);
+            break;
+        }
+        const uint32_t e0 = dt[s0 & smask];
+        uint32_t nb = e0 >> 24;
+        if (br.pos - (int32_t)nb < hdr_bits) {
+            out[o++] = (uint8_t)(e0 >> 16);
+            if (o < n) out[o++] = (uint8_t)(dt[s1 & smask] >> 16);
+            break;
+        }
+        s0 = ((e0 & 0xFFFFu) + br.pop(nb)) & 0xFFFFu;
+        br.refill();
+        out[o++] = (uint8_t)(e0 >> 16);
+        const uint32_t e1 = dt[s1 & smask];
+        nb = e1 >> 24;
+        if (br.pos - (int32_t)nb < hdr_bits) {
+            out[o++] = (uint8_t)(e1 >> 16);
+            if (o < n) out[o++] = (uint8_t)(dt[s0 & smask] >> 16);
+            break;
+        }
+        s1 = ((e1 & 0xFFFFu) + br.pop(nb)) & 0xFFFFu;
+        br.refill();
+        out[o++] = (uint8_t)(e1 >> 16);
+    }
+    return o == n ? FSE_OK : FSE_ERR_LENGTH_MISMATCH;
+}
+
+// One workgroup of NW waves per block.  The compressed block (<= PMAX bytes)
+// is staged into LDS by one coalesced copy; wave 0 parses the header and
+// builds the decode table (fse.rs:280-338) while the block lands; then every
+// lane decodes the checkpoint segments assigned to it.  Without a sidecar
+// (or in reference mode) lane 0 decodes the block serially with every read
+// checked (lib.rs:215-248) and may record the sidecar index.
+template <int LMAX, int NW, uint32_t PMAX>
+struct DecSmem {
+    static constexpr uint32_t SIZE = 1u << LMAX;
+    // dt[i] = new_state | symbol << 16 | nb << 24; the spread scratch lives
+    // in the top half of the same array (see the wave_build_spread call).
+    uint32_t dt[SIZE];
+    uint32_t pay[PMAX / 4];
+    int32_t norm[256];
+    uint16_t cumul[256];
+    uint32_t cnt[256];
+    int scratch[8];
+    int err[NW];
+};
+
+template <int LMAX, int NW, uint32_t PMAX>
+__global__ __launch_bounds__(64 * NW) void decode_blocks_kernel(DecParams P) {
+    __shared__ DecSmem<LMAX, NW, PMAX> sm;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     const uint64_t gb = blockIdx.x;
     if (gb >= P.n_blocks) return;
     const uint8_t* in = P.in + gb * P.slot_bytes;
     const uint32_t clen = P.comp_len[gb];
     const uint64_t ooff = gb * (uint64_t)P.block_size;
-    // raw length: container length, or unknown (reference mode) with cap
+    // raw length: container length, or unknown (reference mode) with a cap
     const bool known = P.n_total != 0;
     const uint32_t n = known ? (uint32_t)min((uint64_t)P.block_size, P.n_total - ooff) : 0u;
     const uint32_t cap = known ? n : P.out_cap;
     uint8_t* out = P.out + ooff;
+    const bool in_lds = clen <= PMAX;
 
-    uint32_t L = 0, tl = 0;
-    if (lane == 0) {
-        int hl = header_read_lane(in, clen, sm.norm, &L, &tl);  // lib.rs:219
-        sm.scratch[0] = hl;
-        sm.scratch[1] = (int)L;
-        sm.scratch[2] = (int)tl;
+    {  // stage the block (or at least its header) in LDS
+        const uint32_t ncopy = in_lds ? clen : min(clen, (uint32_t)min((uint64_t)HDR_MAX, P.slot_bytes));
+        const uint32_t nvec = (ncopy + 15u) >> 4;
+        const uint4* src4 = reinterpret_cast<const uint4*>(in);
+        uint4* dst4 = reinterpret_cast<uint4*>(sm.pay);
+        // LDS-DMA: each wave-instruction moves 1 KiB, lane-linear in LDS
+        for (uint32_t i = wv * 64u; i < nvec; i += 64u * NW) {
+            if (i + lane < nvec)
+                __builtin_amdgcn_global_load_lds(src4 + i + lane, dst4 + i, 16, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
     }
-    __syncthreads();
-    int rc = FSE_OK;
-    const int hl = sm.scratch[0];
-    L = (uint32_t)sm.scratch[1];
-    tl = (uint32_t)sm.scratch[2];
-    if (hl < 0) rc = hl;
-    if (rc == FSE_OK && L > (uint32_t)LMAX) rc = FSE_ERR_UNSUPPORTED;
-    if (rc == FSE_OK && ((uint32_t)hl >= clen || in[clen - 1] == 0)) rc = FSE_ERR_NO_MARKER;  // lib.rs:222
-    const uint32_t size = 1u << L;
-    bool single = false;
-    if (rc == FSE_OK) {
-        uint8_t* scr = reinterpret_cast<uint8_t*>(sm.dt);
-        const int32_t* norm = sm.norm;
-        uint32_t* dt = sm.dt;
-        rc = wave_build_spread(sm.norm, L, tl, scr + 3u * size, scr + 2u * size, sm.cumul, sm.cnt,
-                               [&](uint32_t i, uint32_t s, uint32_t r) {  // fse.rs:329-337
-                                   const int32_t v = norm[s];
-                                   const uint32_t nx = (v == -1 || v < -1 ? 1u : (uint32_t)v) + r;
-                                   const uint32_t nb = L - ilog2u(nx);
-                                   dt[i] = (((nx << nb) - size) & 0xFFFFu) | (s << 16) | (nb << 24);
-                               });
-        for (uint32_t s = lane; s < 256; s += WAVE)
-            if (s < tl && sm.norm[s] == (int32_t)size) single = true;
-        single = __ballot(single) != 0;
-    }
-    __syncthreads();
-    if (rc == FSE_OK && single && !known) rc = FSE_ERR_SINGLE_SYMBOL;
-    if (rc == FSE_OK && known && n < 2) rc = FSE_ERR_LENGTH_MISMATCH;
-    if (rc != FSE_OK) {
+    if (wv == 0) {
+        uint32_t L = 0, tl = 0;
         if (lane == 0) {
+            const int hl = header_read_lane(reinterpret_cast<const uint8_t*>(sm.pay), clen, min(clen, PMAX),
+                                            sm.norm, &L, &tl);  // lib.rs:219
+            sm.scratch[0] = hl;
+            sm.scratch[1] = (int)L;
+            sm.scratch[2] = (int)tl;
+        }
+        wave_sync();
+        int rc = FSE_OK;
+        const int hl = sm.scratch[0];
+        L = (uint32_t)sm.scratch[1];
+        tl = (uint32_t)sm.scratch[2];
+        if (hl < 0) rc = hl;
+        if (rc == FSE_OK && L > (uint32_t)LMAX) rc = FSE_ERR_UNSUPPORTED;
+        if (rc == FSE_OK && ((uint32_t)hl >= clen || in[clen - 1] == 0)) rc = FSE_ERR_NO_MARKER;  // lib.rs:222
+        bool single = false;
+        if (rc == FSE_OK) {
+            const uint32_t size = 1u << L;
+            uint8_t* scr = reinterpret_cast<uint8_t*>(sm.dt);
+            const int32_t* norm = sm.norm;
+            uint32_t* dt = sm.dt;
+            rc = wave_build_spread(sm.norm, L, tl, scr + 3u * size, scr + 2u * size, sm.cumul, sm.cnt,
+                                   [&](uint32_t i, uint32_t s, uint32_t r) {  // fse.rs:329-337
+                                       const int32_t v = norm[s];
+                                       const uint32_t nx = (v == -1 || v < -1 ? 1u : (uint32_t)v) + r;
+                                       const uint32_t nb = L - ilog2u(nx);
+                                       dt[i] = (((nx << nb) - size) & 0xFFFFu) | (s << 16) | (nb << 24);
+                                   });
+            for (uint32_t s = lane; s < 256; s += WAVE)
+                if (s < tl && sm.norm[s] == (int32_t)size) single = true;
+            single = __ballot(single) != 0;
+        }
+        if (rc == FSE_OK && single && !known) rc = FSE_ERR_SINGLE_SYMBOL;
+        if (rc == FSE_OK && known && n < 2) rc = FSE_ERR_LENGTH_MISMATCH;
+        if (lane == 0) sm.scratch[3] = rc;
+    }
+    __syncthreads();
+    const int rc = sm.scratch[3];
+    if (rc != FSE_OK) {
+        if (tid == 0) {
             P.status[gb] = rc;
             if (P.out_len) P.out_len[gb] = 0;
         }
         return;
     }
-    const int32_t hdr_bits = hl * 8;
-    const int32_t top = (int32_t)(clen - 1u) * 8 + (int32_t)ilog2u(in[clen - 1]);
-    const uint32_t* words = reinterpret_cast<const uint32_t*>(in);
+    const int32_t hdr_bits = sm.scratch[0] * 8;
+    const uint32_t L = (uint32_t)sm.scratch[1];
+    const uint32_t smask = (1u << L) - 1u;
     const uint32_t* dt = sm.dt;
-    const uint32_t smask = size - 1u;
+    if (P.debug & 1u) {
+        if (tid == 0) P.status[gb] = FSE_OK;
+        return;
+    }
+    const uint32_t* words = in_lds ? sm.pay : reinterpret_cast<const uint32_t*>(in);
 
     if (P.sidecar && known) {
-        // ---- parallel: lane j decodes checkpoint segments j, j+64, ...
         const uint32_t Pm = (n & 1u) ? (n - 3u) / 2u : n / 2u - 1u;
         const uint32_t I = P.ckpt_interval;
         const uint32_t nseg = Pm / I + 1u;
         const uint64_t* sc = P.sidecar + gb * P.ckpt_per_block;
         int32_t err = FSE_OK;
-        for (uint32_t seg = lane; seg < nseg; seg += WAVE) {
+        for (uint32_t seg = tid; seg < nseg; seg += 64u * NW) {
             const uint64_t e = sc[seg];
-            BitReader br;
+            LdsReader br;
             br.init(words, hdr_bits + (int32_t)(uint32_t)e);
-            uint32_t s0 = (uint32_t)(e >> 32) & 0xFFFFu, s1 = (uint32_t)(e >> 48);
             const uint32_t p0 = seg * I;
             const uint32_t p1 = min(p0 + I, Pm);
-            uint32_t p = p0;
-            // whole 8-pair chunks: 16-byte stores
-            for (; p + 8u <= p1; p += 8u) {
-                uint32_t w[4];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const uint32_t e0 = dt[s0 & smask], e1 = dt[s1 & smask];
-                    const uint32_t nb0 = e0 >> 24;
-                    const uint32_t v0 = br.pop(nb0);
-                    const uint32_t nb1 = e1 >> 24;
-                    const uint32_t v1 = br.pop(nb1);
-                    s0 = ((e0 & 0xFFFFu) + v0) & 0xFFFFu;
-                    s1 = ((e1 & 0xFFFFu) + v1) & 0xFFFFu;
-                    const uint32_t pr = ((e0 >> 16) & 0xFFu) | (e1 & 0xFF0000u) >> 8;
-                    if (j & 1) w[j >> 1] |= pr << 16; else w[j >> 1] = pr;
-                    br.refill();
-                }
-                *reinterpret_cast<uint4*>(out + 2u * p) = make_uint4(w[0], w[1], w[2], w[3]);
-            }
-            for (; p < p1; ++p) {
-                const uint32_t e0 = dt[s0 & smask], e1 = dt[s1 & smask];
-                const uint32_t v0 = br.pop(e0 >> 24);
-                const uint32_t v1 = br.pop(e1 >> 24);
-                s0 = ((e0 & 0xFFFFu) + v0) & 0xFFFFu;
-                s1 = ((e1 & 0xFFFFu) + v1) & 0xFFFFu;
-                out[2u * p] = (uint8_t)(e0 >> 16);
-                out[2u * p + 1u] = (uint8_t)(e1 >> 16);
-                br.refill();
-            }
-            if (seg == nseg - 1u) {
-                // termination in container mode (oracle decompress2_impl),
-                // mirroring lib.rs:227-244
-                uint32_t o = 2u * Pm;
-                for (;;) {
-                    if (o + 2u == n) {
-                        out[o++] = (uint8_t)(dt[s0 & smask] >> 16);
-                        out[o++] = (uint8_t)(dt[s1 & smask] >> 16);
-                        break;
-                    }
-                    if (o + 1u == n) {
-                        out[o++] = (uint8_t)(dt[s0 & smask] >> 16);
-                        break;
-                    }
-                    uint32_t e0 = dt[s0 & smask];
-                    uint32_t nb = e0 >> 24;
-                    if (br.pos - (int32_t)nb < hdr_bits) {
-                        out[o++] = (uint8_t)(e0 >> 16);
-                        if (o < n) out[o++] = (uint8_t)(dt[s1 & smask] >> 16);
-                        break;
-                    }
-                    s0 = ((e0 & 0xFFFFu) + br.pop(nb)) & 0xFFFFu;
-                    br.refill();
-                    out[o++] = (uint8_t)(e0 >> 16);
-                    if (o >= n) { err = FSE_ERR_LENGTH_MISMATCH; break; }
-                    uint32_t e1 = dt[s1 & smask];
-                    nb = e1 >> 24;
-                    if (br.pos - (int32_t)nb < hdr_bits) {
-                        out[o++] = (uint8_t)(e1 >> 16);
-                        if (o < n) out[o++] = (uint8_t)(dt[s0 & smask] >> 16);
-                        break;
-                    }
-                    s1 = ((e1 & 0xFFFFu) + br.pop(nb)) & 0xFFFFu;
-                    br.refill();
-                    out[o++] = (uint8_t)(e1 >> 16);
-                    if (o >= n) { err = FSE_ERR_LENGTH_MISMATCH; break; }
-                }
-                if (o != n) err = FSE_ERR_LENGTH_MISMATCH;
-            }
+            const int32_t r = decode_segment(br, (uint32_t)(e >> 32) & 0xFFFFu, (uint32_t)(e >> 48), p0, p1,
+                                             seg == nseg - 1u, n, Pm, out, dt, smask, hdr_bits);
+            if (r != FSE_OK) err = r;
         }
-        err = (int32_t)wave_max((uint32_t)(-err));
-        if (lane == 0) {
-            P.status[gb] = -err;
-            if (P.out_len) P.out_len[gb] = err ? 0u : n;
+        err = -(int32_t)wave_max((uint32_t)(-err));
+        if (lane == 0) sm.err[wv] = err;
+        __syncthreads();
+        if (tid == 0) {
+            int32_t e = FSE_OK;
+            for (int w = 0; w < NW; ++w)
+                if (sm.err[w] != FSE_OK) e = sm.err[w];
+            P.status[gb] = e;
+            if (P.out_len) P.out_len[gb] = e ? 0u : n;
         }
         return;
     }
 
-    // ---- serial (reference mode or no sidecar): one lane, every read
-    // checked (lib.rs:215-248); optionally records the sidecar index.
-    if (lane != 0) return;
-    BitReader br;
+    // ---- serial (reference mode / no sidecar): lane 0, every read checked
+    if (tid != 0) return;
+    const int32_t top = (int32_t)(clen - 1u) * 8 + (int32_t)ilog2u(in[clen - 1]);
+    LdsReader br;
     br.init(words, top);
     int32_t err = FSE_OK;
     uint32_t o = 0;
@@ -772,20 +846,25 @@ __global__ __launch_bounds__(256) void generate_kernel(GenParams G) {
 // launch wrappers
 // ------------------------------------------------------------------------
 hipError_t launch_encode(const EncParams& P, uint32_t lmax, hipStream_t stream) {
-    const uint32_t grid = (P.n_blocks + 1u) / 2u;  // T = 32 lanes, 2 blocks per workgroup
-    if (lmax <= 11) {
-        hipLaunchKernelGGL((encode_blocks_kernel<11, 32>), dim3(grid), dim3(64), 0, stream, P);
+    const uint32_t T = P.lanes ? P.lanes : 64;
+    const uint32_t bpw = 64u / T;
+    const uint32_t grid = (P.n_blocks + bpw - 1u) / bpw;
+    if (T == 64) {
+        if (lmax <= 11) hipLaunchKernelGGL((encode_blocks_kernel<11, 64>), dim3(grid), dim3(64), 0, stream, P);
+        else hipLaunchKernelGGL((encode_blocks_kernel<12, 64>), dim3(grid), dim3(64), 0, stream, P);
     } else {
-        hipLaunchKernelGGL((encode_blocks_kernel<12, 32>), dim3(grid), dim3(64), 0, stream, P);
+        if (lmax <= 11) hipLaunchKernelGGL((encode_blocks_kernel<11, 32>), dim3(grid), dim3(64), 0, stream, P);
+        else hipLaunchKernelGGL((encode_blocks_kernel<12, 32>), dim3(grid), dim3(64), 0, stream, P);
     }
     return hipGetLastError();
 }
 
 hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) {
+    constexpr uint32_t PM = 40u << 10;  // LDS stage for the compressed block
     if (lmax <= 11) {
-        hipLaunchKernelGGL((decode_blocks_kernel<11>), dim3(P.n_blocks), dim3(64), 0, stream, P);
+        hipLaunchKernelGGL((decode_blocks_kernel<11, 4, PM>), dim3(P.n_blocks), dim3(256), 0, stream, P);
     } else {
-        hipLaunchKernelGGL((decode_blocks_kernel<12>), dim3(P.n_blocks), dim3(64), 0, stream, P);
+        hipLaunchKernelGGL((decode_blocks_kernel<12, 4, PM>), dim3(P.n_blocks), dim3(256), 0, stream, P);
     }
     return hipGetLastError();
 }

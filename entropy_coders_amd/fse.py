@@ -76,7 +76,7 @@ class BlockCodec:
     on torch's current stream.
     """
 
-    def __init__(self, block_size: int = 65536, table_log: int = 0, ckpt_interval: int = 512,
+    def __init__(self, block_size: int = 65536, table_log: int = 0, ckpt_interval: int = 128,
                  device=None):
         import torch
 

@@ -1,0 +1,20 @@
+#!/bin/bash
+# rocprofv3 PMC passes over tools/prof_kernels.py (one counter set per pass,
+# kernel-trace only, as MI355X_MICROARCH.md prescribes).  Output under $1.
+set -e
+OUT=${1:-gpurun_out/pmc}
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+i=0
+while read -r SET; do
+  [ -z "$SET" ] && continue
+  i=$((i+1))
+  timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d $OUT/p$i -o run --pmc $SET -- python3 tools/prof_kernels.py > $OUT/p$i.log 2>&1
+done <<SETS
+SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS
+SQ_LEVEL_WAVES SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU
+FETCH_SIZE
+WRITE_SIZE
+GRBM_GUI_ACTIVE GRBM_COUNT
+SETS
+echo done
