@@ -5,9 +5,9 @@
 // same kernels as the batched API; there is no CPU compute path: without a
 // usable HIP device they return FSE_ERR_NO_DEVICE.
 #include <hip/hip_runtime.h>
-#include <string.h>
-
+#include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <algorithm>
 #include <mutex>
@@ -28,6 +28,42 @@ uint32_t env_u32(const char* name, uint32_t dflt) {
     const char* v = getenv(name);
     return v && *v ? (uint32_t)strtoul(v, nullptr, 0) : dflt;
 }
+
+// FSEHIP_STAMPS=1: per-workgroup phase stamps, averaged and printed to
+// stderr after the (synchronised) launch.  Diagnostics only.
+struct Stamps {
+    uint64_t* d = nullptr;
+    size_t n = 0;
+    uint64_t* get(size_t groups) {
+        if (!env_u32("FSEHIP_STAMPS", 0)) return nullptr;
+        size_t need = groups * fsehip::kStamps;
+        if (n < need) {
+            if (d) (void)hipFree(d);
+            if (hipMalloc(&d, need * 8) != hipSuccess) return d = nullptr;
+            n = need;
+        }
+        (void)hipMemset(d, 0, need * 8);
+        return d;
+    }
+    void report(const char* what, size_t groups, hipStream_t s) {
+        if (!d) return;
+        (void)hipStreamSynchronize(s);
+        std::vector<uint64_t> h(groups * fsehip::kStamps);
+        (void)hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost);
+        double acc[fsehip::kStamps] = {0};
+        size_t cnt[fsehip::kStamps] = {0};
+        for (size_t g = 0; g < groups; ++g)
+            for (int k = 1; k < fsehip::kStamps; ++k) {
+                const uint64_t a = h[g * fsehip::kStamps + k - 1], b = h[g * fsehip::kStamps + k];
+                if (a && b && b >= a) { acc[k] += (double)(b - a); cnt[k]++; }
+            }
+        fprintf(stderr, "[stamps] %s:", what);
+        for (int k = 1; k < fsehip::kStamps; ++k)
+            if (cnt[k]) fprintf(stderr, " %d:%.0f", k, acc[k] / cnt[k]);
+        fprintf(stderr, " (mean cycles per workgroup between stamps k-1 and k)\n");
+    }
+};
+Stamps g_stamps_enc, g_stamps_dec;
 
 bool device_ok() {
     int n = 0;
@@ -167,7 +203,10 @@ int fsehip_compress_blocks(const fsehip_params* p, const uint8_t* d_src, uint64_
     P.status = d_status;
     P.lanes = env_u32("FSEHIP_ENC_LANES", 64) == 32 ? 32 : 64;
     P.debug = env_u32("FSEHIP_DEBUG", 0);
+    const size_t groups = (n_blocks * P.lanes + 63) / 64;
+    P.stamps = g_stamps_enc.get(groups);
     hipError_t e = fsehip::launch_encode(P, lmax, static_cast<hipStream_t>(stream));
+    if (P.stamps) g_stamps_enc.report("encode", groups, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? FSE_OK : FSE_ERR_HIP;
 }
 
@@ -202,7 +241,9 @@ static int decompress_impl(const fsehip_params* p, const uint8_t* d_in, uint64_t
     P.debug = env_u32("FSEHIP_DEBUG", 0) >> 4;
     // the decoder reads L from each header; size its tables for the bound
     uint32_t lmax = p->max_table_log ? p->max_table_log : 12;
+    P.stamps = g_stamps_dec.get(n_blocks);
     hipError_t e = fsehip::launch_decode(P, lmax, static_cast<hipStream_t>(stream));
+    if (P.stamps) g_stamps_dec.report("decode", n_blocks, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? FSE_OK : FSE_ERR_HIP;
 }
 

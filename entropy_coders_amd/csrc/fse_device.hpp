@@ -73,15 +73,21 @@ __device__ __forceinline__ uint64_t match_u8(uint32_t key, uint64_t active) {
 
 // ---------------------------------------------------------------------------
 // Histogram::new (histogram.rs:18-66): 256-bin count of one block by one
-// wave; four LDS sub-histograms (lane & 3) spread same-symbol atomics.
+// wave.  HSUB LDS sub-histograms (lane % HSUB) with a 257-word stride put
+// copies of one bin on different banks, so a skewed block's same-symbol
+// atomics neither serialise on one address nor on one bank.
 // Returns table_len (1 + largest symbol, 1 for an empty block).
 // ---------------------------------------------------------------------------
+constexpr uint32_t HSUB = 4;
+constexpr uint32_t HSTRIDE = 257;
+constexpr uint32_t HIST_WORDS = HSUB * HSTRIDE;
+
 __device__ inline uint32_t wave_histogram(const uint8_t* __restrict__ src, uint32_t n,
-                                          uint32_t* h4 /*LDS [4][256]*/, uint32_t* counts /*LDS[256]*/) {
+                                          uint32_t* hs /*LDS [HIST_WORDS]*/, uint32_t* counts /*LDS[256]*/) {
     const uint32_t lane = lane_id();
-    for (uint32_t i = lane; i < 1024; i += WAVE) h4[i] = 0;
+    for (uint32_t i = lane; i < HIST_WORDS; i += WAVE) hs[i] = 0;
     wave_sync();
-    uint32_t* mine = h4 + (lane & 3u) * 256u;
+    uint32_t* mine = hs + (lane % HSUB) * HSTRIDE;
     uint32_t done = 0;
     if ((reinterpret_cast<uintptr_t>(src) & 15u) == 0) {
         // 8 x 16-byte loads in flight per lane, then count them
@@ -118,7 +124,9 @@ __device__ inline uint32_t wave_histogram(const uint8_t* __restrict__ src, uint3
     wave_sync();
     uint32_t tl = 0;
     for (uint32_t s = lane; s < 256; s += WAVE) {
-        uint32_t c = h4[s] + h4[256 + s] + h4[512 + s] + h4[768 + s];
+        uint32_t c = 0;
+#pragma unroll
+        for (uint32_t h = 0; h < HSUB; ++h) c += hs[h * HSTRIDE + s];
         counts[s] = c;
         if (c) tl = max(tl, s + 1u);
     }
@@ -334,37 +342,150 @@ __device__ inline int header_write_lane(const int32_t* norm, uint32_t L, uint32_
     return (int)len;
 }
 
+// Wave-parallel NormHistogram::write (histogram.rs:376-431), same bytes as
+// header_write_lane.  The writer's state before symbol i depends only on
+// prefix quantities, so every field is placed independently:
+//   remaining_i = 2^L + 1 - sum_{j<i} |norm_j|, threshold_i = the largest
+//   power of two <= remaining_i, nb_i = log2(threshold_i) + 1 (the shrink
+//   loop at 424-427); a zero is written only when it starts a run (391-395);
+//   the 2-bit/16-bit repeat markers for a run of r zeros (r-1 repeats) go
+//   right before the next non-zero symbol (397-408).
+// Field lengths are prefix-summed and the bits OR-ed into the LDS words.
+__device__ __forceinline__ void or_bits(uint32_t* words, uint32_t pos, uint32_t v, uint32_t nb) {
+    if (nb == 0) return;
+    const uint32_t w = pos >> 5, sh = pos & 31u;
+    atomicOr(&words[w], v << sh);
+    if (sh + nb > 32u) atomicOr(&words[w + 1], v >> (32u - sh));
+}
+
+__device__ inline int wave_header_write(const int32_t* norm, uint32_t L, uint32_t tl, uint32_t* hw /*LDS, HDR_MAX/4 words*/) {
+    const uint32_t lane = lane_id();
+    for (uint32_t i = lane; i < HDR_MAX / 4; i += WAVE) hw[i] = 0;
+    int32_t v[4];
+    uint32_t absum = 0, lastnz = 0;  // lastnz: 1 + index of the last non-zero among this lane's symbols
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t i = lane * 4u + k;
+        v[k] = (i < tl) ? norm[i] : 0;
+        absum += (uint32_t)(v[k] < 0 ? -v[k] : v[k]);
+        if (i < tl && v[k] != 0) lastnz = i + 1u;
+    }
+    const uint32_t ex_abs = wave_incl_sum(absum) - absum;
+    const uint32_t prev_nz = max((uint32_t)__shfl_up(wave_incl_max(lastnz), 1, 64), 0u) * (lane ? 1u : 0u);
+    // pass 1: field lengths
+    uint32_t len[4], nbits = 0;
+    {
+        uint32_t rem = (1u << L) + 1u - ex_abs, lnz = prev_nz;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t i = lane * 4u + k;
+            uint32_t l = 0;
+            if (i < tl && rem > 1u) {
+                const bool prev_zero = i > 0 && lnz != i;  // symbol i-1 is zero
+                if (v[k] == 0 && prev_zero) {
+                    l = 0;  // inside a zero run: not written
+                } else {
+                    if (v[k] != 0 && prev_zero) {  // markers for r zeros before i
+                        const uint32_t r = i - lnz;  // lnz = 1 + index of last non-zero
+                        const uint32_t z = r - 1u;
+                        l += 16u * (z / 24u) + 2u * ((z % 24u) / 3u) + 2u;
+                    }
+                    const uint32_t thr = 1u << ilog2u(rem);
+                    const uint32_t nb = ilog2u(thr) + 1u;
+                    const int32_t mx = (int32_t)(2u * thr - 1u - rem);
+                    int32_t c = v[k] + 1;
+                    if (c >= (int32_t)thr) c += mx;
+                    l += nb - (c < mx ? 1u : 0u);
+                }
+            }
+            len[k] = l;
+            nbits += l;
+            rem -= (uint32_t)(v[k] < 0 ? -v[k] : v[k]);
+            if (i < tl && v[k] != 0) lnz = i + 1u;
+        }
+    }
+    const uint32_t ex_bits = wave_incl_sum(nbits) - nbits;
+    const uint32_t total = 4u + __shfl(ex_bits + nbits, 63, 64);
+    const uint32_t bytes = (total + 7u) >> 3;
+    if (bytes > HDR_MAX) return FSE_ERR_DST_TOO_SMALL;
+    wave_sync();
+    // pass 2: place the bits
+    if (lane == 0) or_bits(hw, 0, L - LOG_MIN, 4);
+    {
+        uint32_t pos = 4u + ex_bits;
+        uint32_t rem = (1u << L) + 1u - ex_abs, lnz = prev_nz;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t i = lane * 4u + k;
+            if (len[k]) {
+                const bool prev_zero = i > 0 && lnz != i;
+                if (v[k] != 0 && prev_zero) {
+                    uint32_t z = i - lnz - 1u;
+                    while (z >= 24u) { or_bits(hw, pos, 0xFFFFu, 16); pos += 16; z -= 24u; }
+                    const uint32_t q3 = z / 3u;
+                    if (q3) { or_bits(hw, pos, (1u << (2u * q3)) - 1u, 2u * q3); pos += 2u * q3; }
+                    or_bits(hw, pos, z % 3u, 2);
+                    pos += 2;
+                }
+                const uint32_t thr = 1u << ilog2u(rem);
+                const uint32_t nb = ilog2u(thr) + 1u;
+                const int32_t mx = (int32_t)(2u * thr - 1u - rem);
+                int32_t c = v[k] + 1;
+                if (c >= (int32_t)thr) c += mx;
+                const uint32_t w = nb - (c < mx ? 1u : 0u);
+                or_bits(hw, pos, (uint32_t)c & ((1u << w) - 1u), w);
+                pos += w;
+            }
+            rem -= (uint32_t)(v[k] < 0 ? -v[k] : v[k]);
+            if (i < tl && v[k] != 0) lnz = i + 1u;
+        }
+    }
+    wave_sync();
+    return (int)bytes;
+}
+
 // ---------------------------------------------------------------------------
 // NormHistogram::read (histogram.rs:436-505) + BitStreamReader semantics
 // (stream_reader.rs:16-135), one lane, reading global memory.  Returns the
 // consumed byte count (finish_byte) or < 0.
 // ---------------------------------------------------------------------------
 struct FwdReader {
-    const uint8_t* buf;
-    uint32_t total;  // bits (8 * slice length, stream_reader.rs:16)
+    const uint32_t* w;  // slice as little-endian words
+    uint32_t total;     // bits (8 * slice length, stream_reader.rs:16)
     uint32_t pos;
-    uint32_t avail;  // bytes actually readable at buf (<= total / 8)
-    __device__ bool peek(uint32_t nb, uint32_t* v) const {
+    uint32_t availw;    // words readable at w (bits past them read as 0)
+    uint32_t bufw;      // buf = words bufw, bufw+1
+    uint64_t buf;
+    __device__ __forceinline__ uint32_t load(uint32_t i) const { return i < availw ? w[i] : 0u; }
+    __device__ __forceinline__ void init(const uint32_t* words, uint32_t n_bytes, uint32_t avail_bytes) {
+        w = words;
+        total = n_bytes * 8u;
+        pos = 0;
+        availw = (min(avail_bytes, n_bytes) + 3u) >> 2;
+        bufw = 0;
+        buf = (uint64_t)load(0) | ((uint64_t)load(1) << 32);
+    }
+    __device__ __forceinline__ bool peek(uint32_t nb, uint32_t* v) {
         if (pos + nb > total) return false;
-        uint32_t b = pos >> 3, sh = pos & 7u;
-        uint64_t w = 0;
-        uint32_t nbytes = (sh + nb + 7u) >> 3;
-        for (uint32_t i = 0; i < nbytes; ++i)
-            if (b + i < avail) w |= (uint64_t)buf[b + i] << (8u * i);
-        *v = (uint32_t)((w >> sh) & ((1ull << nb) - 1ull));
+        while (pos >= (bufw + 1u) * 32u) {
+            bufw++;
+            buf = (buf >> 32) | ((uint64_t)load(bufw + 1u) << 32);
+        }
+        *v = (uint32_t)(buf >> (pos - bufw * 32u)) & ((1u << nb) - 1u);
         return true;
     }
-    __device__ bool advance(uint32_t nb) {
+    __device__ __forceinline__ bool advance(uint32_t nb) {
         if (pos + nb > total) return false;
         pos += nb;
         return true;
     }
 };
 
-__device__ inline int header_read_lane(const uint8_t* src, uint32_t n, uint32_t avail, int32_t* norm,
+__device__ inline int header_read_lane(const uint32_t* src, uint32_t n, uint32_t avail, int32_t* norm,
                                        uint32_t* L_out, uint32_t* tl_out) {
     if (n == 0) return FSE_ERR_EMPTY;
-    FwdReader r{src, n * 8u, 0, min(avail, n)};
+    FwdReader r;
+    r.init(src, n, avail);
     uint32_t v;
     if (!r.peek(4, &v)) return FSE_ERR_BAD_HEADER;
     r.advance(4);
@@ -526,6 +647,166 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
         if (act) visit(i, s, r);
         wave_sync();
     }
+    return FSE_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Workgroup version of wave_build_spread for NW waves (decoder tables,
+// fse.rs:280-338): the occurrence max-fill, the spread walk and the rank
+// walk are each split into NW contiguous ranges with cross-wave carries
+// through LDS.  Ranks use per-wave counters, then an exclusive prefix of
+// the counters over waves.  visit(i, s, r) runs after every read of
+// sym_at/occ_sym, so the caller may alias those into its output table.
+// All waves of the workgroup must call it.
+// ---------------------------------------------------------------------------
+template <int NW, int LMAX, typename Visit>
+__device__ inline int block_build_spread(const int32_t* norm, uint32_t L, uint32_t tl, uint8_t* sym_at,
+                                         uint8_t* occ_sym, uint16_t* cumul, uint32_t* cnt /*[NW][256]*/,
+                                         uint32_t* wscr /*[NW + 4]*/, Visit visit) {
+    constexpr uint32_t RMAX = ((1u << LMAX) + 64u * NW - 1u) / (64u * NW);
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    const uint32_t size = 1u << L;
+    const uint32_t mask = size - 1u;
+    for (uint32_t i = tid; i < size; i += 64u * NW) { occ_sym[i] = 0; sym_at[i] = 0; }
+    for (uint32_t i = tid; i < 256u * NW; i += 64u * NW) cnt[i] = 0;
+    __syncthreads();
+    if (wv == 0) {  // per-symbol scans (fse.rs:119-129)
+        uint32_t cp[4], pos_n[4], neg[4];
+        uint32_t sum_c = 0, sum_p = 0, sum_neg = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t s = lane * 4u + k;
+            const int32_t v = (s < tl) ? norm[s] : 0;
+            neg[k] = (v == -1 || v < -1) ? 1u : 0u;
+            pos_n[k] = v > 0 ? (uint32_t)v : 0u;
+            cp[k] = (v == -1) ? 1u : pos_n[k];
+            sum_c += cp[k];
+            sum_p += pos_n[k];
+            sum_neg += neg[k];
+        }
+        const uint32_t ex_c = wave_incl_sum(sum_c) - sum_c;
+        const uint32_t ex_p = wave_incl_sum(sum_p) - sum_p;
+        const uint32_t ex_n = wave_incl_sum(sum_neg) - sum_neg;
+        const uint32_t total_neg = __shfl(ex_n + sum_neg, 63, 64);
+        const uint32_t total_pos = __shfl(ex_p + sum_p, 63, 64);
+        const bool ok = total_pos + total_neg <= size;
+        uint32_t c = ex_c, p = ex_p, ng = ex_n;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t s = lane * 4u + k;
+            cumul[s] = (uint16_t)c;
+            if (ok && pos_n[k]) occ_sym[p] = (uint8_t)s;
+            if (ok && neg[k]) sym_at[size - 1u - ng] = (uint8_t)s;
+            c += cp[k];
+            p += pos_n[k];
+            ng += neg[k];
+        }
+        if (lane == 0) {
+            wscr[NW] = total_pos;
+            wscr[NW + 1] = total_neg;
+            wscr[NW + 2] = ok ? 0u : 1u;
+        }
+    }
+    __syncthreads();
+    const uint32_t total_pos = wscr[NW], total_neg = wscr[NW + 1];
+    if (wscr[NW + 2]) return FSE_ERR_BAD_TABLE;
+    const int32_t ht = (int32_t)size - 1 - (int32_t)total_neg;
+    // occurrence owners: forward max-fill, per-wave ranges + carry
+    const uint32_t orange = ((total_pos + NW - 1u) / NW + 63u) & ~63u;
+    const uint32_t o0 = wv * orange, o1 = min(o0 + orange, total_pos);
+    {
+        uint32_t carry = 0;
+        for (uint32_t base = o0; base < o1; base += WAVE) {
+            const uint32_t j = base + lane;
+            const uint32_t v = (j < o1) ? occ_sym[j] : 0u;
+            const uint32_t f = max(wave_incl_max(v), carry);
+            if (j < o1) occ_sym[j] = (uint8_t)f;
+            carry = __shfl(f, 63, 64);
+        }
+        if (lane == 0) wscr[wv] = carry;
+    }
+    __syncthreads();
+    {
+        uint32_t cin = 0;
+        for (uint32_t w = 0; w < wv; ++w) cin = max(cin, wscr[w]);
+        if (cin)
+            for (uint32_t j = o0 + lane; j < o1; j += WAVE) occ_sym[j] = (uint8_t)max((uint32_t)occ_sym[j], cin);
+    }
+    __syncthreads();
+    // spread (fse.rs:139-151): j-th valid multiplier -> position
+    const uint32_t step = (size >> 3) * 5u + 3u;
+    const uint32_t mrange = (size + NW - 1u) / NW;
+    const uint32_t m0 = wv * mrange, m1 = min(m0 + mrange, size);
+    {
+        uint32_t cntv = 0;
+        for (uint32_t base = m0; base < m1; base += WAVE) {
+            const uint32_t m = base + lane;
+            const bool valid = m < m1 && (int32_t)((m * step) & mask) <= ht;
+            cntv += (uint32_t)__popcll(__ballot(valid));
+        }
+        if (lane == 0) wscr[wv] = cntv;
+    }
+    __syncthreads();
+    {
+        uint32_t j0 = 0, tot = 0;
+        for (uint32_t w = 0; w < NW; ++w) {
+            if (w < wv) j0 += wscr[w];
+            tot += wscr[w];
+        }
+        if (tot != total_pos) return FSE_ERR_BAD_TABLE;  // position != 0 assert
+        for (uint32_t base = m0; base < m1; base += WAVE) {
+            const uint32_t m = base + lane;
+            const uint32_t p = (m * step) & mask;
+            const bool valid = m < m1 && (int32_t)p <= ht;
+            const uint64_t bal = __ballot(valid);
+            const uint32_t j = j0 + (uint32_t)__popcll(bal & lanemask_lt());
+            if (valid) sym_at[p] = occ_sym[j];
+            j0 += (uint32_t)__popcll(bal);
+        }
+    }
+    __syncthreads();
+    // ranks: local ranks per wave range, then per-symbol prefix over waves
+    const uint32_t prange = (size + NW - 1u) / NW;
+    const uint32_t i0 = wv * prange, i1 = min(i0 + prange, size);
+    uint32_t* mycnt = cnt + wv * 256u;
+    uint32_t rs[RMAX];  // local rank << 8 | symbol, per round
+#pragma unroll
+    for (uint32_t r = 0; r < RMAX; ++r) {
+        const uint32_t base = i0 + r * WAVE;
+        rs[r] = 0;
+        if (base < i1) {
+            const uint32_t i = base + lane;
+            const bool act = i < i1;
+            const uint64_t active = __ballot(act);
+            const uint32_t s = act ? sym_at[i] : 0u;
+            const uint64_t peers = match_u8(s, active);
+            const uint32_t before = act ? mycnt[s] : 0u;
+            const uint32_t rk = before + (uint32_t)__popcll(peers & lanemask_lt());
+            wave_sync();
+            if (act && (peers & lanemask_lt()) == 0) mycnt[s] = before + (uint32_t)__popcll(peers);
+            wave_sync();
+            rs[r] = (rk << 8) | s;
+        }
+    }
+    __syncthreads();
+    for (uint32_t s = tid; s < 256u; s += 64u * NW) {
+        uint32_t run = 0;
+        for (uint32_t w = 0; w < NW; ++w) {
+            const uint32_t c = cnt[w * 256u + s];
+            cnt[w * 256u + s] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t r = 0; r < RMAX; ++r) {
+        const uint32_t i = i0 + r * WAVE + lane;
+        if (i0 + r * WAVE < i1 && i < i1) {
+            const uint32_t s = rs[r] & 0xFFu;
+            visit(i, s, (rs[r] >> 8) + mycnt[s]);
+        }
+    }
+    __syncthreads();
     return FSE_OK;
 }
 

@@ -22,6 +22,7 @@ struct EncParams {
     int32_t* status;
     uint32_t lanes;  // encoder lanes per block (32 or 64; 0 = default)
     uint32_t debug;  // ablation: bit0 = tables only, bit1 = no emit pass
+    uint64_t* stamps;  // diagnostics: per-workgroup s_memtime at phase ends
 };
 
 struct DecParams {
@@ -40,6 +41,7 @@ struct DecParams {
     uint32_t* out_len;
     uint64_t* sidecar_out;  // serial mode: record checkpoints here
     uint32_t debug;         // ablation: bit0 = header + table only
+    uint64_t* stamps;       // diagnostics: per-workgroup s_memtime at phase ends
 };
 
 struct GenParams {
@@ -51,6 +53,8 @@ struct GenParams {
     uint32_t nsym;
     uint16_t bound[1024];
 };
+
+constexpr int kStamps = 10;  // stamp slots per workgroup
 
 hipError_t launch_encode(const EncParams& P, uint32_t lmax, hipStream_t stream);
 hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream);

@@ -24,6 +24,12 @@ namespace fsehip {
 // ------------------------------------------------------------------------
 // small helpers
 // ------------------------------------------------------------------------
+// Diagnostic phase stamps (only when P.stamps is set by the host).
+#define FSE_STAMP(P, slot)                                                                     \
+    do {                                                                                       \
+        if ((P).stamps && threadIdx.x == 0)                                                    \
+            (P).stamps[(uint64_t)blockIdx.x * kStamps + (slot)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
 __device__ __forceinline__ uint4 load_chunk(const uint8_t* blk, uint32_t n, uint32_t c) {
     const uint32_t off = c << 4;
     if (off + 16u <= n) return *reinterpret_cast<const uint4*>(blk + off);
@@ -105,15 +111,23 @@ template <int MODE, bool FULL>
 __device__ __forceinline__ void enc_chunk(const uint4& q, uint32_t c8, uint32_t pb, uint32_t& x0, uint32_t& x1,
                                           const EncTab& T, uint32_t& bits, Emit& em) {
     const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+    // all 16 symbol transforms depend only on the chunk: issue their LDS
+    // reads up front so only the stateTable reads sit on the state chain
+    uint2 t0[8], t1[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint32_t sh = 16u * (uint32_t)(j & 1);
+        t0[j] = T.tt[(w[j >> 1] >> sh) & 0xFFu];
+        t1[j] = T.tt[(w[j >> 1] >> (sh + 8u)) & 0xFFu];
+    }
 #pragma unroll
     for (int j = 7; j >= 0; --j) {
         if (!FULL && c8 + (uint32_t)j >= pb) continue;
-        const uint32_t sh = 16u * (uint32_t)(j & 1);
-        const uint32_t s0 = (w[j >> 1] >> sh) & 0xFFu;
-        const uint32_t s1 = (w[j >> 1] >> (sh + 8u)) & 0xFFu;
         const uint32_t v1 = x1, v0 = x0;
-        const uint32_t nb1 = enc_step(x1, s1, T);
-        const uint32_t nb0 = enc_step(x0, s0, T);
+        const uint32_t nb1 = (t1[j].x + x1) >> 16;
+        x1 = *reinterpret_cast<const uint16_t*>(T.st + ((x1 >> nb1) << 1) + (int32_t)t1[j].y);
+        const uint32_t nb0 = (t0[j].x + x0) >> 16;
+        x0 = *reinterpret_cast<const uint16_t*>(T.st + ((x0 >> nb0) << 1) + (int32_t)t0[j].y);
         if (MODE == PASS_COUNT) bits += nb1 + nb0;
         if (MODE == PASS_EMIT) {
             const uint32_t pairbits = (v1 & ((1u << nb1) - 1u)) | ((v0 & ((1u << nb0) - 1u)) << nb1);
@@ -215,9 +229,9 @@ struct EncSmem {
     static constexpr uint32_t SIZE = 1u << LMAX;
     uint16_t st[BPW][SIZE];
     uint2 tt[BPW][256];
-    uint8_t hdr[BPW][HDR_MAX];
+    uint32_t hdrw[BPW][HDR_MAX / 4];
     union {
-        uint32_t h4[1024];
+        uint32_t hs[HIST_WORDS];
         struct {
             uint8_t sym_at[SIZE];
             uint8_t occ_sym[SIZE];
@@ -243,6 +257,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     __shared__ EncSmem<LMAX, T> sm;
     const uint32_t lane = lane_id();
 
+    FSE_STAMP(P, 0);
     // ---- phase 1: statistics, header and tables, one block at a time
     for (int b = 0; b < BPW; ++b) {
         const uint64_t gb = (uint64_t)blockIdx.x * BPW + b;
@@ -253,7 +268,8 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
         const uint64_t off = gb * P.block_size;
         const uint32_t n = (uint32_t)min((uint64_t)P.block_size, P.n_total - off);
         const uint8_t* blk = P.src + off;
-        const uint32_t tl = wave_histogram(blk, n, sm.tmp.h4, sm.counts);
+        const uint32_t tl = wave_histogram(blk, n, sm.tmp.hs, sm.counts);
+        FSE_STAMP(P, 1);
         int rc = FSE_OK;
         uint32_t Lreq = P.table_log, L = 0, slow = 0;
         if (n == 0) rc = FSE_ERR_EMPTY;
@@ -261,11 +277,13 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
         if (rc == FSE_OK) rc = wave_normalize(sm.counts, n, tl, Lreq, sm.norm, &L, &slow, sm.scratch);
         if (rc == FSE_OK && n < 2) rc = FSE_ERR_TOO_SHORT;  // lib.rs:154/156 unwrap
         if (rc == FSE_OK && L > (uint32_t)LMAX) rc = FSE_ERR_UNSUPPORTED;
+        FSE_STAMP(P, 2);
         if (rc == FSE_OK) {
-            if (lane == 0) sm.scratch[1] = header_write_lane(sm.norm, L, tl, sm.hdr[b]);
-            __syncthreads();
-            if (sm.scratch[1] < 0) rc = sm.scratch[1];
+            const int hl = wave_header_write(sm.norm, L, tl, sm.hdrw[b]);
+            if (lane == 0) sm.scratch[1] = hl;
+            if (hl < 0) rc = hl;
         }
+        FSE_STAMP(P, 3);
         if (rc == FSE_OK) {
             const uint32_t size = 1u << L;
             uint16_t* st = sm.st[b];
@@ -307,6 +325,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
         __syncthreads();
     }
 
+    FSE_STAMP(P, 4);
     if (P.debug & 1u) return;  // ablation: statistics + tables only
     // ---- phase 2: T lanes per block
     const int b = BPW == 1 ? 0 : (int)(lane / T);
@@ -337,6 +356,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     }
     __syncthreads();
 
+    FSE_STAMP(P, 5);
     // count pass from the neighbour's spec end state, then verify: a lane's
     // start must equal its neighbour's exact end state.  Iterating to the
     // unique fixed point (the top lane is exact) makes every lane exact.
@@ -364,6 +384,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
         need = bad;
     }
 
+    FSE_STAMP(P, 6);
     // offsets: lane k writes after every lane j > k (stack order)
     const uint32_t hl = sm.info_hl[b];
     const uint32_t hdr_bits = hl * 8u;
@@ -426,7 +447,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     }
     // header: whole words stored directly, the last partial word merged
     if (live && fits) {
-        const uint8_t* h = sm.hdr[b];
+        const uint8_t* h = reinterpret_cast<const uint8_t*>(sm.hdrw[b]);
         for (uint32_t w = k; w < hl / 4u; w += T)
             gw[w] = (uint32_t)h[4 * w] | ((uint32_t)h[4 * w + 1] << 8) | ((uint32_t)h[4 * w + 2] << 16) |
                     ((uint32_t)h[4 * w + 3] << 24);
@@ -437,6 +458,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
             sm.mval[b][0] = v;
         }
     }
+    FSE_STAMP(P, 7);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stores above land before the merge rewrites
     __syncthreads();
     // merge: each run of equal word indices is OR-ed by its first entry
@@ -463,6 +485,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
             gw[w] = v;
         }
     }
+    FSE_STAMP(P, 8);
     if (live && k == 0) {
         if (fits) {
             P.status[gb] = FSE_OK;
@@ -597,7 +620,8 @@ struct DecSmem {
     uint32_t pay[PMAX / 4];
     int32_t norm[256];
     uint16_t cumul[256];
-    uint32_t cnt[256];
+    uint32_t cnt[NW * 256];
+    uint32_t wscr[NW + 4];
     int scratch[8];
     int err[NW];
 };
@@ -617,6 +641,7 @@ __global__ __launch_bounds__(64 * NW) void decode_blocks_kernel(DecParams P) {
     const uint32_t cap = known ? n : P.out_cap;
     uint8_t* out = P.out + ooff;
     const bool in_lds = clen <= PMAX;
+    FSE_STAMP(P, 0);
 
     {  // stage the block (or at least its header) in LDS
         const uint32_t ncopy = in_lds ? clen : min(clen, (uint32_t)min((uint64_t)HDR_MAX, P.slot_bytes));
@@ -631,45 +656,45 @@ __global__ __launch_bounds__(64 * NW) void decode_blocks_kernel(DecParams P) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
-    if (wv == 0) {
+    FSE_STAMP(P, 1);
+    if (tid == 0) {  // NormHistogram::read (lib.rs:219)
         uint32_t L = 0, tl = 0;
-        if (lane == 0) {
-            const int hl = header_read_lane(reinterpret_cast<const uint8_t*>(sm.pay), clen, min(clen, PMAX),
-                                            sm.norm, &L, &tl);  // lib.rs:219
-            sm.scratch[0] = hl;
-            sm.scratch[1] = (int)L;
-            sm.scratch[2] = (int)tl;
-        }
-        wave_sync();
-        int rc = FSE_OK;
-        const int hl = sm.scratch[0];
-        L = (uint32_t)sm.scratch[1];
-        tl = (uint32_t)sm.scratch[2];
-        if (hl < 0) rc = hl;
+        const int hl = header_read_lane(sm.pay, clen, min(clen, PMAX), sm.norm, &L, &tl);
+        int rc = hl < 0 ? hl : FSE_OK;
         if (rc == FSE_OK && L > (uint32_t)LMAX) rc = FSE_ERR_UNSUPPORTED;
         if (rc == FSE_OK && ((uint32_t)hl >= clen || in[clen - 1] == 0)) rc = FSE_ERR_NO_MARKER;  // lib.rs:222
-        bool single = false;
-        if (rc == FSE_OK) {
-            const uint32_t size = 1u << L;
-            uint8_t* scr = reinterpret_cast<uint8_t*>(sm.dt);
-            const int32_t* norm = sm.norm;
-            uint32_t* dt = sm.dt;
-            rc = wave_build_spread(sm.norm, L, tl, scr + 3u * size, scr + 2u * size, sm.cumul, sm.cnt,
-                                   [&](uint32_t i, uint32_t s, uint32_t r) {  // fse.rs:329-337
-                                       const int32_t v = norm[s];
-                                       const uint32_t nx = (v == -1 || v < -1 ? 1u : (uint32_t)v) + r;
-                                       const uint32_t nb = L - ilog2u(nx);
-                                       dt[i] = (((nx << nb) - size) & 0xFFFFu) | (s << 16) | (nb << 24);
-                                   });
-            for (uint32_t s = lane; s < 256; s += WAVE)
-                if (s < tl && sm.norm[s] == (int32_t)size) single = true;
-            single = __ballot(single) != 0;
-        }
-        if (rc == FSE_OK && single && !known) rc = FSE_ERR_SINGLE_SYMBOL;
-        if (rc == FSE_OK && known && n < 2) rc = FSE_ERR_LENGTH_MISMATCH;
-        if (lane == 0) sm.scratch[3] = rc;
+        sm.scratch[0] = hl;
+        sm.scratch[1] = (int)L;
+        sm.scratch[2] = (int)tl;
+        sm.scratch[3] = rc;
     }
     __syncthreads();
+    FSE_STAMP(P, 2);
+    if (sm.scratch[3] == FSE_OK) {  // DecodeTable::update (lib.rs:223, fse.rs:280-338)
+        const uint32_t L = (uint32_t)sm.scratch[1], tl = (uint32_t)sm.scratch[2];
+        const uint32_t size = 1u << L;
+        uint8_t* scr = reinterpret_cast<uint8_t*>(sm.dt);
+        const int32_t* norm = sm.norm;
+        uint32_t* dt = sm.dt;
+        const int r = block_build_spread<NW, LMAX>(sm.norm, L, tl, scr + 3u * size, scr + 2u * size, sm.cumul,
+                                                   sm.cnt, sm.wscr, [&](uint32_t i, uint32_t s, uint32_t rk) {
+                                                       const int32_t v = norm[s];
+                                                       const uint32_t nx = (v == -1 || v < -1 ? 1u : (uint32_t)v) + rk;
+                                                       const uint32_t nb = L - ilog2u(nx);
+                                                       dt[i] = (((nx << nb) - size) & 0xFFFFu) | (s << 16) | (nb << 24);
+                                                   });
+        if (tid == 0) {
+            int rc = r;
+            bool single = false;
+            for (uint32_t q = 0; q < tl; ++q)
+                if (sm.norm[q] == (int32_t)size) single = true;
+            if (rc == FSE_OK && single && !known) rc = FSE_ERR_SINGLE_SYMBOL;
+            if (rc == FSE_OK && known && n < 2) rc = FSE_ERR_LENGTH_MISMATCH;
+            sm.scratch[3] = rc;
+        }
+    }
+    __syncthreads();
+    FSE_STAMP(P, 3);
     const int rc = sm.scratch[3];
     if (rc != FSE_OK) {
         if (tid == 0) {
@@ -686,7 +711,7 @@ __global__ __launch_bounds__(64 * NW) void decode_blocks_kernel(DecParams P) {
         if (tid == 0) P.status[gb] = FSE_OK;
         return;
     }
-    const uint32_t* words = in_lds ? sm.pay : reinterpret_cast<const uint32_t*>(in);
+    const uint32_t* gwords = reinterpret_cast<const uint32_t*>(in);
 
     if (P.sidecar && known) {
         const uint32_t Pm = (n & 1u) ? (n - 3u) / 2u : n / 2u - 1u;
@@ -696,17 +721,25 @@ __global__ __launch_bounds__(64 * NW) void decode_blocks_kernel(DecParams P) {
         int32_t err = FSE_OK;
         for (uint32_t seg = tid; seg < nseg; seg += 64u * NW) {
             const uint64_t e = sc[seg];
-            LdsReader br;
-            br.init(words, hdr_bits + (int32_t)(uint32_t)e);
             const uint32_t p0 = seg * I;
             const uint32_t p1 = min(p0 + I, Pm);
-            const int32_t r = decode_segment(br, (uint32_t)(e >> 32) & 0xFFFFu, (uint32_t)(e >> 48), p0, p1,
-                                             seg == nseg - 1u, n, Pm, out, dt, smask, hdr_bits);
+            int32_t r;
+            LdsReader br;  // LDS and global instantiations stay separate (no flat loads)
+            if (in_lds) {
+                br.init(sm.pay, hdr_bits + (int32_t)(uint32_t)e);
+                r = decode_segment(br, (uint32_t)(e >> 32) & 0xFFFFu, (uint32_t)(e >> 48), p0, p1,
+                                   seg == nseg - 1u, n, Pm, out, dt, smask, hdr_bits);
+            } else {
+                br.init(gwords, hdr_bits + (int32_t)(uint32_t)e);
+                r = decode_segment(br, (uint32_t)(e >> 32) & 0xFFFFu, (uint32_t)(e >> 48), p0, p1,
+                                   seg == nseg - 1u, n, Pm, out, dt, smask, hdr_bits);
+            }
             if (r != FSE_OK) err = r;
         }
         err = -(int32_t)wave_max((uint32_t)(-err));
         if (lane == 0) sm.err[wv] = err;
         __syncthreads();
+        FSE_STAMP(P, 4);
         if (tid == 0) {
             int32_t e = FSE_OK;
             for (int w = 0; w < NW; ++w)
@@ -721,7 +754,7 @@ __global__ __launch_bounds__(64 * NW) void decode_blocks_kernel(DecParams P) {
     if (tid != 0) return;
     const int32_t top = (int32_t)(clen - 1u) * 8 + (int32_t)ilog2u(in[clen - 1]);
     LdsReader br;
-    br.init(words, top);
+    br.init(gwords, top);  // serial path reads global memory (rare; any length)
     int32_t err = FSE_OK;
     uint32_t o = 0;
     if (br.pos - (int32_t)L < hdr_bits) err = FSE_ERR_TOO_SHORT;  // lib.rs:224
@@ -787,7 +820,7 @@ __global__ __launch_bounds__(64 * NW) void decode_blocks_kernel(DecParams P) {
 __global__ __launch_bounds__(64) void histogram_blocks_kernel(const uint8_t* src, uint64_t n_total,
                                                               uint32_t block_size, uint32_t n_blocks,
                                                               uint32_t* counts, uint32_t* table_len) {
-    __shared__ uint32_t h4[1024];
+    __shared__ uint32_t h4[HIST_WORDS];
     __shared__ uint32_t cnts[256];
     const uint64_t gb = blockIdx.x;
     if (gb >= n_blocks) return;
@@ -860,7 +893,7 @@ hipError_t launch_encode(const EncParams& P, uint32_t lmax, hipStream_t stream) 
 }
 
 hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) {
-    constexpr uint32_t PM = 40u << 10;  // LDS stage for the compressed block
+    constexpr uint32_t PM = 39u << 10;  // LDS stage for the compressed block (3 workgroups/CU at L<=11)
     if (lmax <= 11) {
         hipLaunchKernelGGL((decode_blocks_kernel<11, 4, PM>), dim3(P.n_blocks), dim3(256), 0, stream, P);
     } else {
