@@ -39,6 +39,9 @@ def parse():
     ap.add_argument("--ckpt", type=int, default=128)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--gather", action="store_true",
+                    help="after the timed steps, pack each rank's blocks on the GPU and gather the "
+                         "compressed streams to rank 0 (RCCL); reported separately, never in value")
     return ap.parse_args()
 
 
@@ -173,6 +176,24 @@ def main():
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         ok = bool(flag.item())
 
+    gather_info = None
+    if args.gather:
+        from entropy_coders_amd.dist import gather_stream, pack_device
+
+        torch.cuda.synchronize(dev)
+        barrier()
+        g0 = time.perf_counter()
+        packed, _ = pack_device(cb["out"], codec.slot_bytes, cb["comp_len"])
+        tp = time.perf_counter()
+        if world > 1:
+            streams, _ = gather_stream(packed, cb["comp_len"], dst=0)
+        torch.cuda.synchronize(dev)
+        g1 = time.perf_counter()
+        gather_info = {"packed_bytes_per_rank": int(packed.numel()),
+                       "pack_plus_gather_ms": round((g1 - g0) * 1e3, 3),
+                       "gather_GB_s": round(world * packed.numel() / max(g1 - tp, 1e-9) / 1e9, 2)
+                       if world > 1 else None}
+
     if rank == 0:
         enc_bytes = n + comp_bytes + side_bytes  # raw read + compressed (+ sidecar) written
         dec_bytes = comp_bytes + side_bytes + n  # compressed (+ sidecar) read + raw written
@@ -225,6 +246,8 @@ def main():
             "compressed_ratio": round(comp_bytes / n, 5),
             "verified_roundtrip": ok,
         }
+        if gather_info is not None:
+            line["gather"] = gather_info
         if world == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(src.cpu().numpy(), args.block, args.cpu_seconds)
         print(json.dumps(line), flush=True)

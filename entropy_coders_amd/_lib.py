@@ -18,6 +18,7 @@ EXPORTS = (
     "fsehip_slot_bytes", "fsehip_sidecar_per_block", "fsehip_compress_blocks",
     "fsehip_decompress_blocks", "fsehip_build_sidecar", "fsehip_histogram_blocks",
     "fsehip_generate", "fsehip_device_count", "fsehip_version",
+    "fsehip_pack_blocks", "fsehip_unpack_blocks",
 )
 
 STATUS = {
@@ -67,6 +68,8 @@ def load() -> C.CDLL:
     lib.fsehip_build_sidecar.argtypes = [C.POINTER(Params), P, u64, P, P, u64, P, P, P]
     lib.fsehip_histogram_blocks.argtypes = [P, u64, u32, P, P, P]
     lib.fsehip_generate.argtypes = [C.c_int, C.c_double, u64, u32, P, u64, P]
+    lib.fsehip_pack_blocks.argtypes = [P, u64, P, P, u32, P, P]
+    lib.fsehip_unpack_blocks.argtypes = [P, P, P, u32, P, u64, P]
     lib.fsehip_device_count.argtypes = []
     lib.fsehip_version.restype = C.c_char_p
     for name in EXPORTS:

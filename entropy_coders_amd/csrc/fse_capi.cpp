@@ -276,6 +276,26 @@ int fsehip_histogram_blocks(const uint8_t* d_src, uint64_t n_total, uint32_t blo
     return e == hipSuccess ? FSE_OK : FSE_ERR_HIP;
 }
 
+int fsehip_pack_blocks(const uint8_t* d_slots, uint64_t slot_bytes, const uint32_t* d_comp_len,
+                       const uint64_t* d_offsets, uint32_t n_blocks, uint8_t* d_stream, fsehip_stream_t stream) {
+    if (!d_slots || !d_comp_len || !d_offsets || !d_stream || (slot_bytes & 15u)) return FSE_ERR_BAD_ARG;
+    if (n_blocks == 0) return FSE_OK;
+    if (!device_ok()) return FSE_ERR_NO_DEVICE;
+    hipError_t e = fsehip::launch_pack(d_slots, slot_bytes, d_comp_len, d_offsets, n_blocks, d_stream, 0,
+                                       static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? FSE_OK : FSE_ERR_HIP;
+}
+
+int fsehip_unpack_blocks(const uint8_t* d_stream, const uint64_t* d_offsets, const uint32_t* d_comp_len,
+                         uint32_t n_blocks, uint8_t* d_slots, uint64_t slot_bytes, fsehip_stream_t stream) {
+    if (!d_slots || !d_comp_len || !d_offsets || !d_stream || (slot_bytes & 15u)) return FSE_ERR_BAD_ARG;
+    if (n_blocks == 0) return FSE_OK;
+    if (!device_ok()) return FSE_ERR_NO_DEVICE;
+    hipError_t e = fsehip::launch_pack(d_slots, slot_bytes, d_comp_len, d_offsets, n_blocks,
+                                       const_cast<uint8_t*>(d_stream), 1, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? FSE_OK : FSE_ERR_HIP;
+}
+
 int fsehip_generate(int kind, double prob, uint64_t seed, uint32_t block_size, uint8_t* d_out, uint64_t n_total,
                     fsehip_stream_t stream) {
     if (!d_out || kind < 0 || kind > 2) return FSE_ERR_BAD_ARG;

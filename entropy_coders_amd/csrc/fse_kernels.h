@@ -61,5 +61,7 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream);
 hipError_t launch_histogram(const uint8_t* src, uint64_t n_total, uint32_t block_size, uint32_t n_blocks,
                             uint32_t* counts, uint32_t* table_len, hipStream_t stream);
 hipError_t launch_generate(const GenParams& G, hipStream_t stream);
+hipError_t launch_pack(const uint8_t* slots, uint64_t slot_bytes, const uint32_t* comp_len, const uint64_t* offsets,
+                       uint32_t n_blocks, uint8_t* stream, int unpack, hipStream_t hs);
 
 }  // namespace fsehip

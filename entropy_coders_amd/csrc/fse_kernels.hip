@@ -832,6 +832,34 @@ __global__ __launch_bounds__(64) void histogram_blocks_kernel(const uint8_t* src
 }
 
 // ------------------------------------------------------------------------
+// Pack / unpack between the per-block slot layout and one contiguous
+// stream (blocks back to back, byte offsets from an exclusive scan of the
+// compressed lengths).  One 256-thread workgroup per block; offsets are
+// arbitrary, so the copy is done in bytes with 16-byte source reads.
+// ------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void pack_blocks_kernel(const uint8_t* __restrict__ slots, uint64_t slot_bytes,
+                                                          const uint32_t* __restrict__ comp_len,
+                                                          const uint64_t* __restrict__ offsets, uint32_t n_blocks,
+                                                          uint8_t* __restrict__ stream, int unpack) {
+    const uint64_t b = blockIdx.x;
+    if (b >= n_blocks) return;
+    const uint32_t len = comp_len[b];
+    uint8_t* slot = const_cast<uint8_t*>(slots) + b * slot_bytes;
+    uint8_t* s = stream + offsets[b];
+    if (!unpack) {
+        for (uint32_t i = threadIdx.x * 16u; i < len; i += 256u * 16u) {
+            const uint4 v = *reinterpret_cast<const uint4*>(slot + i);
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (uint32_t k = 0; k < 16u; ++k)
+                if (i + k < len) s[i + k] = (uint8_t)(w[k >> 2] >> (8u * (k & 3u)));
+        }
+    } else {
+        for (uint32_t i = threadIdx.x; i < len; i += 256u) slot[i] = s[i];
+    }
+}
+
+// ------------------------------------------------------------------------
 // Synthetic generator (same definition as oracle fo_generate).
 // ------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
@@ -906,6 +934,13 @@ hipError_t launch_histogram(const uint8_t* src, uint64_t n_total, uint32_t block
                             uint32_t* counts, uint32_t* table_len, hipStream_t stream) {
     hipLaunchKernelGGL(histogram_blocks_kernel, dim3(n_blocks), dim3(64), 0, stream, src, n_total, block_size,
                        n_blocks, counts, table_len);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack(const uint8_t* slots, uint64_t slot_bytes, const uint32_t* comp_len, const uint64_t* offsets,
+                       uint32_t n_blocks, uint8_t* stream, int unpack, hipStream_t hs) {
+    hipLaunchKernelGGL(pack_blocks_kernel, dim3(n_blocks), dim3(256), 0, hs, slots, slot_bytes, comp_len, offsets,
+                       n_blocks, stream, unpack);
     return hipGetLastError();
 }
 

@@ -98,6 +98,14 @@ int fsehip_build_sidecar(const fsehip_params* p, const uint8_t* d_in, uint64_t s
                          const uint32_t* d_comp_len, uint8_t* d_out, uint64_t n_total, uint64_t* d_sidecar_out,
                          int32_t* d_status, fsehip_stream_t stream);
 
+/* Compact the slot layout into one stream (blocks back to back at the byte
+ * offsets d_offsets[b], an exclusive scan of d_comp_len) and back.  Used to
+ * ship compressed shards between GPUs (RCCL gather) or to the host. */
+int fsehip_pack_blocks(const uint8_t* d_slots, uint64_t slot_bytes, const uint32_t* d_comp_len,
+                       const uint64_t* d_offsets, uint32_t n_blocks, uint8_t* d_stream, fsehip_stream_t stream);
+int fsehip_unpack_blocks(const uint8_t* d_stream, const uint64_t* d_offsets, const uint32_t* d_comp_len,
+                         uint32_t n_blocks, uint8_t* d_slots, uint64_t slot_bytes, fsehip_stream_t stream);
+
 /* histogram::count per block: d_counts[b*256 + s], d_table_len[b]. */
 int fsehip_histogram_blocks(const uint8_t* d_src, uint64_t n_total, uint32_t block_size, uint32_t* d_counts,
                             uint32_t* d_table_len, fsehip_stream_t stream);

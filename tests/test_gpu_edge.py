@@ -1,0 +1,135 @@
+"""GPU edge cases against the oracle: sparse alphabets (zero runs in the
+NCount header), ragged/degenerate blocks inside one batch, per-block error
+statuses, and the pack/unpack compaction used by the multi-GPU gather."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+BLOCK = 4096
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def _sparse(rng, syms, n, weights=None):
+    syms = np.asarray(syms, dtype=np.uint8)
+    p = None if weights is None else np.asarray(weights, float) / np.sum(weights)
+    return syms[rng.choice(len(syms), size=n, p=p)]
+
+
+def _edge_blocks():
+    rng = np.random.default_rng(1234)
+    blocks = [
+        _sparse(rng, [5, 200, 255], BLOCK),                        # long zero runs in the header
+        _sparse(rng, [0, 255], BLOCK, [1, 3]),                     # 254-symbol zero run
+        _sparse(rng, [1, 2], BLOCK, [1, 1000]),                    # one very rare symbol
+        _sparse(rng, list(range(0, 256, 17)), BLOCK),              # periodic gaps
+        _sparse(rng, list(range(256)), BLOCK),                     # full alphabet
+        _sparse(rng, [0, 3, 4, 5, 6, 7, 8, 200], BLOCK, [50, 1, 1, 1, 1, 1, 1, 5]),  # repeat flags
+        np.full(BLOCK, 9, np.uint8),                               # single symbol (container mode)
+        np.zeros(BLOCK, np.uint8),                                 # ALL_ZERO_SYMBOL0 (reference panic)
+        (np.arange(BLOCK) % 256).astype(np.uint8),                 # flat
+        _sparse(rng, [7, 8], BLOCK, [1, 1]),
+    ]
+    return blocks
+
+
+def test_sparse_host_api(torch_cuda):
+    from entropy_coders_amd import compress2, decompress2
+
+    for i, s in enumerate(_edge_blocks()):
+        try:
+            want, wbits = O.compress2(s)
+        except O.OracleError as e:
+            from entropy_coders_amd import FseError
+            with pytest.raises(FseError) as g:
+                compress2(s)
+            assert g.value.code == e.code
+            continue
+        got, bits = compress2(s)
+        assert got == want and bits == wbits, i
+        if len(set(s.tolist())) > 1:
+            assert decompress2(got) == s.tobytes(), i
+    for L in (9, 10, 12):
+        s = _edge_blocks()[0]
+        assert compress2_log_eq(s, L)
+
+
+def compress2_log_eq(s, L):
+    from entropy_coders_amd import compress2_log
+
+    return compress2_log(s, L)[0] == O.compress2(s, L)[0]
+
+
+@pytest.mark.parametrize("ckpt", [0, 64, 128])
+def test_edge_batch(torch_cuda, ckpt):
+    torch = torch_cuda
+    from entropy_coders_amd import BlockCodec
+    from entropy_coders_amd._lib import STATUS
+
+    blocks = _edge_blocks()
+    tail = blocks[0][:1000]
+    host = np.concatenate(blocks + [tail])
+    codec = BlockCodec(block_size=BLOCK, ckpt_interval=ckpt)
+    src = torch.from_numpy(host).cuda()
+    cb = codec.compress(src)
+    out, st = codec.decompress(cb)
+    torch.cuda.synchronize()
+    est = cb["status"].cpu().numpy()
+    dst = st.cpu().numpy()
+    outh = out.cpu().numpy()
+    for b, s in enumerate(blocks + [tail]):
+        try:
+            want, wbits = O.compress2(s)
+        except O.OracleError as e:
+            assert STATUS.get(int(est[b])) == e.code, b
+            assert dst[b] != 0, b
+            continue
+        assert est[b] == 0, b
+        assert codec.block_bytes(cb, b) == want, b
+        assert int(cb["payload_bits"][b]) == wbits, b
+        assert dst[b] == 0, (b, dst[b])
+        assert np.array_equal(outh[b * BLOCK: b * BLOCK + len(s)], s), b
+
+
+def test_pack_unpack(torch_cuda):
+    torch = torch_cuda
+    from entropy_coders_amd import BlockCodec
+    from entropy_coders_amd.dist import pack_device, pack_host
+
+    codec = BlockCodec(block_size=65536, ckpt_interval=128)
+    n = 37 * 65536 + 999
+    src = codec.generate(0, 0.3, 99, n)
+    cb = codec.compress(src)
+    stream, offs = pack_device(cb["out"], codec.slot_bytes, cb["comp_len"])
+    torch.cuda.synchronize()
+    ref, roffs = pack_host(cb["out"].cpu(), codec.slot_bytes, cb["comp_len"].cpu())
+    assert torch.equal(stream.cpu(), ref) and torch.equal(offs.cpu(), roffs)
+    nb = codec.n_blocks(n)
+    for b in (0, 17, nb - 1):
+        o = int(offs[b])
+        assert stream[o: o + int(cb["comp_len"][b])].cpu().numpy().tobytes() == codec.block_bytes(cb, b)
+    # unpack into fresh slots, then decode from them
+    import ctypes as C
+    from entropy_coders_amd._lib import check, load
+
+    lib = load()
+    cb2 = codec.alloc(n)
+    cb2["comp_len"].copy_(cb["comp_len"])
+    cb2["sidecar"].copy_(cb["sidecar"])
+    hs = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    check(lib.fsehip_unpack_blocks(C.c_void_p(stream.data_ptr()), C.c_void_p(offs.data_ptr()),
+                                   C.c_void_p(cb["comp_len"].data_ptr()), nb, C.c_void_p(cb2["out"].data_ptr()),
+                                   codec.slot_bytes, hs))
+    out, st = codec.decompress(cb2)
+    torch.cuda.synchronize()
+    assert int(st.abs().max()) == 0 and torch.equal(out, src)
