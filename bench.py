@@ -205,7 +205,8 @@ def main():
         if os.path.exists(tpath):
             try:
                 with open(tpath) as f:
-                    traffic = json.load(f).get(dom[0])
+                    t = json.load(f).get(dom[0])
+                traffic = int(t["bytes_per_launch"]) if t else None
             except Exception:
                 traffic = None
         line = {
@@ -237,6 +238,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_source": "profiles/traffic.json: rocprofv3 FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, per launch",
                 "algorithmic_bytes_per_launch": dom[2],
             },
             "encode_ms": round(enc_ms, 4),
