@@ -19,6 +19,7 @@ EXPORTS = (
     "fsehip_decompress_blocks", "fsehip_build_sidecar", "fsehip_histogram_blocks",
     "fsehip_generate", "fsehip_device_count", "fsehip_version",
     "fsehip_pack_blocks", "fsehip_unpack_blocks",
+    "fsehip_dtable_bytes", "fsehip_build_dtables", "fsehip_decompress_blocks_dt",
 )
 
 STATUS = {
@@ -66,6 +67,10 @@ def load() -> C.CDLL:
     lib.fsehip_compress_blocks.argtypes = [C.POINTER(Params), P, u64, P, u64, P, P, P, P, P]
     lib.fsehip_decompress_blocks.argtypes = [C.POINTER(Params), P, u64, P, P, P, u64, P, P]
     lib.fsehip_build_sidecar.argtypes = [C.POINTER(Params), P, u64, P, P, u64, P, P, P]
+    lib.fsehip_dtable_bytes.argtypes = [u32]
+    lib.fsehip_dtable_bytes.restype = u64
+    lib.fsehip_build_dtables.argtypes = [C.POINTER(Params), P, u64, P, u32, P, P, P]
+    lib.fsehip_decompress_blocks_dt.argtypes = [C.POINTER(Params), P, u64, P, P, P, P, P, u64, P, P]
     lib.fsehip_histogram_blocks.argtypes = [P, u64, u32, P, P, P]
     lib.fsehip_generate.argtypes = [C.c_int, C.c_double, u64, u32, P, u64, P]
     lib.fsehip_pack_blocks.argtypes = [P, u64, P, P, u32, P, P]

@@ -213,7 +213,8 @@ int fsehip_compress_blocks(const fsehip_params* p, const uint8_t* d_src, uint64_
 static int decompress_impl(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
                            const uint32_t* d_comp_len, const uint64_t* d_sidecar, uint8_t* d_out, uint64_t n_total,
                            uint64_t* d_sidecar_out, int32_t* d_status, uint32_t* d_out_len, uint32_t out_cap,
-                           fsehip_stream_t stream) {
+                           fsehip_stream_t stream, const uint32_t* d_dt = nullptr,
+                           const int32_t* d_dtinfo = nullptr) {
     if (!p || !d_in || !d_comp_len || !d_out || !d_status) return FSE_ERR_BAD_ARG;
     const uint32_t bs = p->block_size ? p->block_size : kDefaultBlock;
     const uint64_t n_blocks = n_total ? (n_total + bs - 1) / bs : 1;
@@ -239,19 +240,113 @@ static int decompress_impl(const fsehip_params* p, const uint8_t* d_in, uint64_t
     P.out_len = d_out_len;
     P.sidecar_out = d_sidecar_out;
     P.debug = env_u32("FSEHIP_DEBUG", 0) >> 4;
+    P.waves = env_u32("FSEHIP_DEC_WAVES", 4) == 8 ? 8 : 4;
     // the decoder reads L from each header; size its tables for the bound
     uint32_t lmax = p->max_table_log ? p->max_table_log : 12;
+    P.dt = d_dt;
+    P.dtinfo = d_dtinfo;
     P.stamps = g_stamps_dec.get(n_blocks);
     hipError_t e = fsehip::launch_decode(P, lmax, static_cast<hipStream_t>(stream));
     if (P.stamps) g_stamps_dec.report("decode", n_blocks, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? FSE_OK : FSE_ERR_HIP;
 }
 
+static uint32_t dt_lmax(const fsehip_params* p) { return (p && p->max_table_log && p->max_table_log <= 11) ? 11 : 12; }
+
+uint64_t fsehip_dtable_bytes(uint32_t max_table_log) {
+    return 4ull << ((max_table_log && max_table_log <= 11) ? 11 : 12);
+}
+
+int fsehip_build_dtables(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes, const uint32_t* d_comp_len,
+                         uint32_t n_blocks, uint32_t* d_dtables, int32_t* d_dtinfo, fsehip_stream_t stream) {
+    if (!p || !d_in || !d_comp_len || !d_dtables || !d_dtinfo || (slot_bytes & 255u)) return FSE_ERR_BAD_ARG;
+    if (n_blocks == 0) return FSE_OK;
+    if (!device_ok()) return FSE_ERR_NO_DEVICE;
+    fsehip::DtParams D{};
+    D.in = d_in;
+    D.slot_bytes = slot_bytes;
+    D.comp_len = d_comp_len;
+    D.n_blocks = n_blocks;
+    D.dt = d_dtables;
+    D.dtinfo = d_dtinfo;
+    hipError_t e = fsehip::launch_dtables(D, dt_lmax(p), static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? FSE_OK : FSE_ERR_HIP;
+}
+
+int fsehip_decompress_blocks_dt(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
+                                const uint32_t* d_comp_len, const uint64_t* d_sidecar, const uint32_t* d_dtables,
+                                const int32_t* d_dtinfo, uint8_t* d_out, uint64_t n_total, int32_t* d_status,
+                                fsehip_stream_t stream) {
+    if (n_total == 0) return FSE_ERR_EMPTY;
+    if (!p || !d_sidecar || !d_dtables || !d_dtinfo || p->ckpt_interval == 0) return FSE_ERR_BAD_ARG;
+    fsehip_params q = *p;
+    q.max_table_log = dt_lmax(p);  // the table stride the tables were built with
+    return decompress_impl(&q, d_in, slot_bytes, d_comp_len, d_sidecar, d_out, n_total, nullptr, d_status, nullptr,
+                           0, stream, d_dtables, d_dtinfo);
+}
+
+// Per-(device, stream) decode-table workspace of the two-kernel decode
+// behind fsehip_decompress_blocks: calls on one stream are ordered, calls on
+// different streams get different buffers.  Grow-only.
+namespace {
+struct DtWorkspace {
+    uint32_t* dt = nullptr;
+    int32_t* info = nullptr;
+    uint64_t blocks = 0;
+    uint32_t lmax = 0;
+};
+std::mutex g_ws_mu;
+std::vector<std::pair<std::pair<int, void*>, DtWorkspace>> g_ws;
+
+DtWorkspace* workspace(void* stream, uint64_t n_blocks, uint32_t lmax) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    DtWorkspace* w = nullptr;
+    for (auto& kv : g_ws)
+        if (kv.first.first == dev && kv.first.second == stream) w = &kv.second;
+    if (!w) {
+        g_ws.push_back({{dev, stream}, DtWorkspace{}});
+        w = &g_ws.back().second;
+    }
+    if (w->blocks < n_blocks || w->lmax < lmax) {
+        if (w->dt) {
+            (void)hipStreamSynchronize(static_cast<hipStream_t>(stream));
+            (void)hipFree(w->dt);
+            (void)hipFree(w->info);
+            w->dt = nullptr;
+            w->info = nullptr;
+        }
+        w->blocks = std::max(w->blocks, n_blocks);
+        w->lmax = std::max(w->lmax, lmax);
+        if (hipMalloc(&w->dt, (4ull << w->lmax) * w->blocks) != hipSuccess ||
+            hipMalloc(&w->info, 4ull * w->blocks) != hipSuccess) {
+            w->blocks = 0;
+            return nullptr;
+        }
+    }
+    return w;
+}
+}  // namespace
+
 int fsehip_decompress_blocks(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
                              const uint32_t* d_comp_len, const uint64_t* d_sidecar, uint8_t* d_out, uint64_t n_total,
                              int32_t* d_status, fsehip_stream_t stream) {
     if (n_total == 0) return FSE_ERR_EMPTY;
     if (d_sidecar && p && p->ckpt_interval == 0) return FSE_ERR_BAD_ARG;
+    if (d_sidecar && p && !env_u32("FSEHIP_DEC_FUSED", 0)) {
+        // two kernels: decode tables for all blocks at high occupancy, then
+        // the LDS-heavy segment decode with no serial phase
+        const uint32_t bs = p->block_size ? p->block_size : kDefaultBlock;
+        const uint64_t n_blocks = (n_total + bs - 1) / bs;
+        if (!device_ok()) return FSE_ERR_NO_DEVICE;
+        DtWorkspace* w = workspace(stream, n_blocks, dt_lmax(p));
+        if (!w) return FSE_ERR_HIP;
+        int rc = fsehip_build_dtables(p, d_in, slot_bytes, d_comp_len, (uint32_t)n_blocks, w->dt, w->info, stream);
+        if (rc != FSE_OK) return rc;
+        return fsehip_decompress_blocks_dt(p, d_in, slot_bytes, d_comp_len, d_sidecar, w->dt, w->info, d_out,
+                                           n_total, d_status, stream);
+    }
     return decompress_impl(p, d_in, slot_bytes, d_comp_len, d_sidecar, d_out, n_total, nullptr, d_status, nullptr,
                            0, stream);
 }

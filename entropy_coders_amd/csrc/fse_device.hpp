@@ -544,6 +544,103 @@ __device__ inline int header_read_lane(const uint32_t* src, uint32_t n, uint32_t
 }
 
 // ---------------------------------------------------------------------------
+// NormHistogram::read (histogram.rs:436-505) as wave-uniform code: every lane
+// of the calling wave holds the same values, so the serial parse runs on the
+// scalar unit (s_lshr_b64 window, s_flbit for the threshold) instead of one
+// VALU lane.  Words come from LDS through readfirstlane.  norm[] must be
+// zeroed by the caller; lane 0 stores the parsed entries.  Same results and
+// statuses as header_read_lane.
+// ---------------------------------------------------------------------------
+__device__ inline int header_read_wave(uint32_t r0, uint32_t r1, uint32_t n, uint32_t lmax, int32_t* norm,
+                                       uint32_t* L_out, uint32_t* tl_out) {
+    if (n == 0) return FSE_ERR_EMPTY;
+    const uint32_t lane = lane_id();
+    const int32_t total = (int32_t)(n * 8u);
+    // r0 / r1 hold header words lane / 64 + lane (zero past the block): a
+    // word is one v_readlane.  Headers of L <= 12 fit in 417 bytes, so the
+    // 512 bytes held always cover them (L > lmax returns before reading on).
+    auto ld = [&](uint32_t i) -> uint32_t {
+        const uint32_t a = __builtin_amdgcn_readlane(r0, i & 63u);
+        const uint32_t b = __builtin_amdgcn_readlane(r1, i & 63u);
+        return i < 64u ? a : (i < 128u ? b : 0u);
+    };
+    // window: words bw, bw+1; next bit = 32*bw + off; left = bits after it
+    uint32_t bw = 0, off = 0;
+    int32_t left = total;
+    uint64_t buf = (uint64_t)ld(0) | ((uint64_t)ld(1) << 32);
+    auto refill = [&]() {  // fields are <= 16 bits, so one word per field suffices
+        if (off >= 32u) {
+            off -= 32u;
+            ++bw;
+            buf = (buf >> 32) | ((uint64_t)ld(bw + 1u) << 32);
+        }
+    };
+    if (left < 4) return FSE_ERR_BAD_HEADER;
+    const uint32_t L = ((uint32_t)buf & 15u) + LOG_MIN;
+    off = 4;
+    left -= 4;
+    if (L > LOG_MAX_REF) return FSE_ERR_BAD_HEADER;  // TableLogTooLarge
+    if (L > lmax) return FSE_ERR_UNSUPPORTED;          // valid for the crate, beyond this build's tables
+    uint32_t sym = 0, rem = (1u << L) + 1u, lg = L, thr = 1u << L;  // read width = lg + 1
+    bool prev0 = false;
+    while (rem > 1u && sym < 256u) {
+        if (prev0) {  // zero-run marks (456-464): peek(..).unwrap_or(0)
+            for (;;) {
+                refill();
+                if (left < 16 || ((uint32_t)(buf >> off) & 0xFFFFu) != 0xFFFFu) break;
+                off += 16u;
+                left -= 16;
+                sym += 24u;
+            }
+            for (;;) {
+                refill();
+                if (left < 2 || ((uint32_t)(buf >> off) & 3u) != 3u) break;
+                off += 2u;
+                left -= 2;
+                sym += 3u;
+            }
+            if (left < 2) return FSE_ERR_BAD_HEADER;
+            sym += (uint32_t)(buf >> off) & 3u;
+            off += 2u;
+            left -= 2;
+            if (sym >= 256u) break;
+        }
+        refill();
+        // peek(nb) falling back to peek(nb-1) (471-473): the short path only
+        // uses the low nb-1 bits, and the long path needs all nb, so one
+        // bound check on the advance covers both
+        const uint32_t raw = (uint32_t)(buf >> off);
+        const uint32_t mx = (2u * thr - 1u) - rem;
+        const uint32_t low = raw & (thr - 1u);
+        uint32_t val, adv;
+        if (low < mx) {
+            adv = lg;
+            val = low;
+        } else {
+            adv = lg + 1u;
+            val = raw & (2u * thr - 1u);
+            if (val >= thr) val -= mx;
+        }
+        if (left < (int32_t)adv) return FSE_ERR_BAD_HEADER;
+        off += adv;
+        left -= (int32_t)adv;
+        const int32_t sv = (int32_t)val - 1;
+        rem -= (uint32_t)(sv < 0 ? -sv : sv);
+        if (lane == 0) norm[sym] = sv;
+        sym += 1u;
+        prev0 = sv == 0;
+        if (rem < thr) {  // the halving loop of 492-495 in closed form
+            lg = ilog2u(rem);
+            thr = 1u << lg;
+        }
+    }
+    if (rem != 1u) return FSE_ERR_BAD_HEADER;  // TooManySymbols
+    *L_out = L;
+    *tl_out = sym;
+    return (total - left + 7) >> 3;
+}
+
+// ---------------------------------------------------------------------------
 // Symbol spread and per-position occurrence rank (fse.rs:110-162, 294-337),
 // wave-parallel.  After the call:
 //   sym_at[i]  = symbol at table position i            (LDS, 2^L bytes)

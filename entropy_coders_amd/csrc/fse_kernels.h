@@ -42,6 +42,19 @@ struct DecParams {
     uint64_t* sidecar_out;  // serial mode: record checkpoints here
     uint32_t debug;         // ablation: bit0 = header + table only
     uint64_t* stamps;       // diagnostics: per-workgroup s_memtime at phase ends
+    uint32_t waves;         // waves per block workgroup: 4 (default) or 8
+    const uint32_t* dt;     // prebuilt decode tables [n_blocks][1 << lmax], or nullptr
+    const int32_t* dtinfo;  // per block: header bytes | L << 16, or < 0 = status
+};
+
+// Decode-table build (header parse + DecodeTable) for a batch of blocks.
+struct DtParams {
+    const uint8_t* in;
+    uint64_t slot_bytes;
+    const uint32_t* comp_len;
+    uint32_t n_blocks;
+    uint32_t* dt;      // [n_blocks][1 << lmax] entries (dte_make layout)
+    int32_t* dtinfo;   // header bytes | L << 16, or < 0 = status
 };
 
 struct GenParams {
@@ -57,6 +70,7 @@ struct GenParams {
 constexpr int kStamps = 10;  // stamp slots per workgroup
 
 hipError_t launch_encode(const EncParams& P, uint32_t lmax, hipStream_t stream);
+hipError_t launch_dtables(const DtParams& P, uint32_t lmax, hipStream_t stream);
 hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream);
 hipError_t launch_histogram(const uint8_t* src, uint64_t n_total, uint32_t block_size, uint32_t n_blocks,
                             uint32_t* counts, uint32_t* table_len, hipStream_t stream);

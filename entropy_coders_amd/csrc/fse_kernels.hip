@@ -540,46 +540,37 @@ __device__ __forceinline__ void store_byte(uint8_t* out, uint32_t i, uint32_t li
     if (i < lim) out[i] = (uint8_t)v;
 }
 
+// Decode table entry (fse.rs:260-265 DecodeTransform, repacked for the
+// decode loop): nb | symbol << 8 | (4 * new_state) << 16.  nb in bits 0-4
+// lets an entry serve directly as a v_bfe width/offset operand, the byte
+// sum of two entries' low bytes is nb0 + nb1, and the high half is the LDS
+// byte offset of the next state's base entry.
+__device__ __forceinline__ uint32_t dte_make(uint32_t nb, uint32_t sym, uint32_t ns) {
+    return nb | (sym << 8) | (ns << 18);
+}
+__device__ __forceinline__ uint32_t dte_nb(uint32_t e) { return e & 0xFFu; }
+__device__ __forceinline__ uint32_t dte_sym(uint32_t e) { return (e >> 8) & 0xFFu; }
+__device__ __forceinline__ uint32_t dte_ns(uint32_t e) { return e >> 18; }
+
 // Decode main-loop pairs [p0, p1) of one segment without read checks (the
-// sidecar guarantees the bits), 8 pairs per 16-byte store; when `last`,
-// finish with the reference termination in container mode (the oracle's
-// decompress2_impl; lib.rs:227-244).  Returns a status.
+// sidecar guarantees the bits) through a windowed reader (global-memory
+// blocks); when `last`, finish with the reference termination in container
+// mode (the oracle's decompress2_impl; lib.rs:227-244).  Returns a status.
 template <class RD>
 __device__ __forceinline__ int32_t decode_segment(RD& br, uint32_t s0, uint32_t s1, uint32_t p0, uint32_t p1,
                                                   bool last, uint32_t n, uint32_t Pm, uint8_t* __restrict__ out,
                                                   const uint32_t* dt, uint32_t smask, int32_t hdr_bits) {
     uint32_t p = p0;
-    // 32 pairs = one whole 64-byte memory segment per lane, stored back to
-    // back: HBM writes in full 64 B bursts instead of four masked 16 B ones
-    // (the 16 B-per-chunk form measured ~4x WRITE_SIZE).
-    for (; p + DEC_GROUP <= p1; p += DEC_GROUP) {
-        uint32_t w[DEC_GROUP / 2u];
-#pragma unroll
-        for (int j = 0; j < (int)DEC_GROUP; ++j) {
-            const uint32_t e0 = dt[s0 & smask], e1 = dt[s1 & smask];
-            const uint32_t v0 = br.pop(e0 >> 24);
-            const uint32_t v1 = br.pop(e1 >> 24);
-            s0 = ((e0 & 0xFFFFu) + v0) & 0xFFFFu;
-            s1 = ((e1 & 0xFFFFu) + v1) & 0xFFFFu;
-            const uint32_t pr = ((e0 >> 16) & 0xFFu) | ((e1 >> 8) & 0xFF00u);
-            if (j & 1) w[j >> 1] |= pr << 16; else w[j >> 1] = pr;
-            br.refill();
-        }
-        uint4* o4 = reinterpret_cast<uint4*>(out + 2u * p);
-#pragma unroll
-        for (uint32_t q = 0; q < DEC_GROUP / 8u; ++q)
-            o4[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
-    }
     for (; p + 8u <= p1; p += 8u) {
         uint32_t w[4];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const uint32_t e0 = dt[s0 & smask], e1 = dt[s1 & smask];
-            const uint32_t v0 = br.pop(e0 >> 24);
-            const uint32_t v1 = br.pop(e1 >> 24);
-            s0 = ((e0 & 0xFFFFu) + v0) & 0xFFFFu;
-            s1 = ((e1 & 0xFFFFu) + v1) & 0xFFFFu;
-            const uint32_t pr = ((e0 >> 16) & 0xFFu) | ((e1 >> 8) & 0xFF00u);
+            const uint32_t v0 = br.pop(dte_nb(e0));
+            const uint32_t v1 = br.pop(dte_nb(e1));
+            s0 = dte_ns(e0) + v0;
+            s1 = dte_ns(e1) + v1;
+            const uint32_t pr = __builtin_amdgcn_perm(e1, e0, 0x0c0c0501u);
             if (j & 1) w[j >> 1] |= pr << 16; else w[j >> 1] = pr;
             br.refill();
         }
@@ -587,46 +578,135 @@ __device__ __forceinline__ int32_t decode_segment(RD& br, uint32_t s0, uint32_t 
     }
     for (; p < p1; ++p) {
         const uint32_t e0 = dt[s0 & smask], e1 = dt[s1 & smask];
-        const uint32_t v0 = br.pop(e0 >> 24);
-        const uint32_t v1 = br.pop(e1 >> 24);
-        s0 = ((e0 & 0xFFFFu) + v0) & 0xFFFFu;
-        s1 = ((e1 & 0xFFFFu) + v1) & 0xFFFFu;
-        out[2u * p] = (uint8_t)(e0 >> 16);
-        out[2u * p + 1u] = (uint8_t)(e1 >> 16);
+        const uint32_t v0 = br.pop(dte_nb(e0));
+        const uint32_t v1 = br.pop(dte_nb(e1));
+        s0 = dte_ns(e0) + v0;
+        s1 = dte_ns(e1) + v1;
+        out[2u * p] = (uint8_t)dte_sym(e0);
+        out[2u * p + 1u] = (uint8_t)dte_sym(e1);
         br.refill();
     }
     if (!last) return FSE_OK;
     uint32_t o = 2u * Pm;
     for (;;) {
         if (o + 2u == n) {
-            out[o++] = (uint8_t)(dt[s0 & smask] >> 16);
-            out[o++] = (uint8_t)(dt[s1 & smask] >> 16);
+            out[o++] = (uint8_t)dte_sym(dt[s0 & smask]);
+            out[o++] = (uint8_t)dte_sym(dt[s1 & smask]);
             break;
         }
         if (o + 1u == n) {
-            out[o++] = (uint8_t)(dt[s0 & smask] >> 16);
+            out[o++] = (uint8_t)dte_sym(dt[s0 & smask]);
             break;
         }
         const uint32_t e0 = dt[s0 & smask];
-        uint32_t nb = e0 >> 24;
+        uint32_t nb = dte_nb(e0);
         if (br.pos - (int32_t)nb < hdr_bits) {
-            out[o++] = (uint8_t)(e0 >> 16);
-            if (o < n) out[o++] = (uint8_t)(dt[s1 & smask] >> 16);
+            out[o++] = (uint8_t)dte_sym(e0);
+            if (o < n) out[o++] = (uint8_t)dte_sym(dt[s1 & smask]);
             break;
         }
-        s0 = ((e0 & 0xFFFFu) + br.pop(nb)) & 0xFFFFu;
+        s0 = dte_ns(e0) + br.pop(nb);
         br.refill();
-        out[o++] = (uint8_t)(e0 >> 16);
+        out[o++] = (uint8_t)dte_sym(e0);
         const uint32_t e1 = dt[s1 & smask];
-        nb = e1 >> 24;
+        nb = dte_nb(e1);
         if (br.pos - (int32_t)nb < hdr_bits) {
-            out[o++] = (uint8_t)(e1 >> 16);
-            if (o < n) out[o++] = (uint8_t)(dt[s0 & smask] >> 16);
+            out[o++] = (uint8_t)dte_sym(e1);
+            if (o < n) out[o++] = (uint8_t)dte_sym(dt[s0 & smask]);
             break;
         }
-        s1 = ((e1 & 0xFFFFu) + br.pop(nb)) & 0xFFFFu;
+        s1 = dte_ns(e1) + br.pop(nb);
         br.refill();
-        out[o++] = (uint8_t)(e1 >> 16);
+        out[o++] = (uint8_t)dte_sym(e1);
+    }
+    return o == n ? FSE_OK : FSE_ERR_LENGTH_MISMATCH;
+}
+
+// Bits [pos, pos + 32) of an LDS-staged block (pos >= 0): one ds_read2 of
+// the two words holding them and a v_alignbit.  Bits above the block's end
+// are garbage; callers only use the low nb0 + nb1 <= 24 bits.
+__device__ __forceinline__ uint32_t lds_bits32(const uint32_t* pay, int32_t pos) {
+    const uint32_t* wp = pay + ((uint32_t)pos >> 5);
+    return __builtin_amdgcn_alignbit(wp[1], wp[0], (uint32_t)pos);
+}
+
+// The same segment decode for a block staged in LDS, with absolute bit
+// addressing and no reader state: per pair, pos -= nb0 + nb1 (byte sum of
+// the two entries), one 32-bit window at pos, then v1 = low nb1 bits and
+// v0 = the nb0 bits above (stack order: decoder 0 pops first), and the next
+// states' LDS offsets.  32 pairs = one whole 64-byte segment per lane are
+// stored back to back (full HBM write bursts).  `a0`/`a1` are LDS byte
+// offsets of the current states' entries.
+__device__ __forceinline__ int32_t decode_segment_lds(const uint32_t* pay, int32_t pos, uint32_t s0, uint32_t s1,
+                                                      uint32_t p0, uint32_t p1, bool last, uint32_t n, uint32_t Pm,
+                                                      uint8_t* __restrict__ out, const uint32_t* dt,
+                                                      int32_t hdr_bits) {
+    const uint8_t* dtb = reinterpret_cast<const uint8_t*>(dt);
+    uint32_t a0 = s0 << 2, a1 = s1 << 2;
+    auto pair = [&]() -> uint32_t {
+        const uint32_t e0 = *reinterpret_cast<const uint32_t*>(dtb + a0);
+        const uint32_t e1 = *reinterpret_cast<const uint32_t*>(dtb + a1);
+        pos -= (int32_t)((e0 + e1) & 0xFFu);
+        const uint32_t x = lds_bits32(pay, pos);
+        const uint32_t v1 = __builtin_amdgcn_ubfe(x, 0u, e1);
+        const uint32_t v0 = __builtin_amdgcn_ubfe(x, e1, e0);
+        a0 = (e0 >> 16) + (v0 << 2);
+        a1 = (e1 >> 16) + (v1 << 2);
+        return __builtin_amdgcn_perm(e1, e0, 0x0c0c0501u);  // sym0 | sym1 << 8
+    };
+    uint32_t p = p0;
+    for (; p + DEC_GROUP <= p1; p += DEC_GROUP) {
+        uint32_t w[DEC_GROUP / 2u];
+#pragma unroll
+        for (uint32_t j = 0; j < DEC_GROUP; j += 2u) {
+            const uint32_t lo = pair();
+            const uint32_t hi = pair();
+            w[j >> 1] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);  // lo.b0 lo.b1 hi.b0 hi.b1
+        }
+        uint4* o4 = reinterpret_cast<uint4*>(out + 2u * p);
+#pragma unroll
+        for (uint32_t q = 0; q < DEC_GROUP / 8u; ++q)
+            o4[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+    }
+    for (; p < p1; ++p) {
+        const uint32_t pr = pair();
+        out[2u * p] = (uint8_t)pr;
+        out[2u * p + 1u] = (uint8_t)(pr >> 8);
+    }
+    if (!last) return FSE_OK;
+    // container-mode termination (lib.rs:227-244 with the raw length known)
+    auto ent = [&](uint32_t a) { return *reinterpret_cast<const uint32_t*>(dtb + a); };
+    uint32_t o = 2u * Pm;
+    for (;;) {
+        if (o + 2u == n) {
+            out[o++] = (uint8_t)dte_sym(ent(a0));
+            out[o++] = (uint8_t)dte_sym(ent(a1));
+            break;
+        }
+        if (o + 1u == n) {
+            out[o++] = (uint8_t)dte_sym(ent(a0));
+            break;
+        }
+        const uint32_t e0 = ent(a0);
+        uint32_t nb = dte_nb(e0);
+        if (pos - (int32_t)nb < hdr_bits) {
+            out[o++] = (uint8_t)dte_sym(e0);
+            if (o < n) out[o++] = (uint8_t)dte_sym(ent(a1));
+            break;
+        }
+        pos -= (int32_t)nb;
+        a0 = (e0 >> 16) + (__builtin_amdgcn_ubfe(lds_bits32(pay, pos), 0u, nb) << 2);
+        out[o++] = (uint8_t)dte_sym(e0);
+        const uint32_t e1 = ent(a1);
+        nb = dte_nb(e1);
+        if (pos - (int32_t)nb < hdr_bits) {
+            out[o++] = (uint8_t)dte_sym(e1);
+            if (o < n) out[o++] = (uint8_t)dte_sym(ent(a0));
+            break;
+        }
+        pos -= (int32_t)nb;
+        a1 = (e1 >> 16) + (__builtin_amdgcn_ubfe(lds_bits32(pay, pos), 0u, nb) << 2);
+        out[o++] = (uint8_t)dte_sym(e1);
     }
     return o == n ? FSE_OK : FSE_ERR_LENGTH_MISMATCH;
 }
@@ -640,10 +720,10 @@ __device__ __forceinline__ int32_t decode_segment(RD& br, uint32_t s0, uint32_t 
 template <int LMAX, int NW, uint32_t PMAX>
 struct DecSmem {
     static constexpr uint32_t SIZE = 1u << LMAX;
-    // dt[i] = new_state | symbol << 16 | nb << 24; the spread scratch lives
+    // dt[i] = dte_make(nb, symbol, new_state); the spread scratch lives
     // in the top half of the same array (see the wave_build_spread call).
+    uint32_t pay[PMAX / 4];  // first: LDS offset 0, so payload addresses need no base add
     uint32_t dt[SIZE];
-    uint32_t pay[PMAX / 4];
     int32_t norm[256];
     uint16_t cumul[256];
     uint32_t cnt[NW * 256];
@@ -667,11 +747,14 @@ __global__ __launch_bounds__(64 * NW) void decode_blocks_kernel(DecParams P) {
     const uint32_t cap = known ? n : P.out_cap;
     uint8_t* out = P.out + ooff;
     const bool in_lds = clen <= PMAX;
+    // prebuilt decode tables (dtable_blocks_kernel / C3): no header parse, no table build
+    const bool pre = P.dt != nullptr;
+    const int32_t info = pre ? P.dtinfo[gb] : 0;
     FSE_STAMP(P, 0);
 
-    {  // stage the block (or at least its header) in LDS
+    {  // stage the block (or at least its header) in LDS, plus a prebuilt table
         const uint32_t ncopy = in_lds ? clen : min(clen, (uint32_t)min((uint64_t)HDR_MAX, P.slot_bytes));
-        const uint32_t nvec = (ncopy + 15u) >> 4;
+        const uint32_t nvec = (pre && info < 0) ? 0u : (ncopy + 15u) >> 4;
         const uint4* src4 = reinterpret_cast<const uint4*>(in);
         uint4* dst4 = reinterpret_cast<uint4*>(sm.pay);
         // LDS-DMA: each wave-instruction moves 1 KiB, lane-linear in LDS
@@ -679,49 +762,76 @@ __global__ __launch_bounds__(64 * NW) void decode_blocks_kernel(DecParams P) {
             if (i + lane < nvec)
                 __builtin_amdgcn_global_load_lds(src4 + i + lane, dst4 + i, 16, 0, 0);
         }
+        if (pre && info >= 0) {
+            const uint32_t dvec = 1u << ((uint32_t)info >> 16) >> 2;  // 4 << L bytes
+            const uint4* t4 = reinterpret_cast<const uint4*>(P.dt + gb * (uint64_t)(1u << LMAX));
+            uint4* d4 = reinterpret_cast<uint4*>(sm.dt);
+            for (uint32_t i = wv * 64u; i < dvec; i += 64u * NW) {
+                if (i + lane < dvec)
+                    __builtin_amdgcn_global_load_lds(t4 + i + lane, d4 + i, 16, 0, 0);
+            }
+        }
+        if (!pre)
+            for (uint32_t i = tid; i < 256u; i += 64u * NW) sm.norm[i] = 0;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
     FSE_STAMP(P, 1);
-    if (tid == 0) {  // NormHistogram::read (lib.rs:219)
-        uint32_t L = 0, tl = 0;
-        const int hl = header_read_lane(sm.pay, clen, min(clen, PMAX), sm.norm, &L, &tl);
-        int rc = hl < 0 ? hl : FSE_OK;
-        if (rc == FSE_OK && L > (uint32_t)LMAX) rc = FSE_ERR_UNSUPPORTED;
-        if (rc == FSE_OK && ((uint32_t)hl >= clen || in[clen - 1] == 0)) rc = FSE_ERR_NO_MARKER;  // lib.rs:222
-        sm.scratch[0] = hl;
-        sm.scratch[1] = (int)L;
-        sm.scratch[2] = (int)tl;
-        sm.scratch[3] = rc;
-    }
-    __syncthreads();
-    FSE_STAMP(P, 2);
-    if (sm.scratch[3] == FSE_OK) {  // DecodeTable::update (lib.rs:223, fse.rs:280-338)
-        const uint32_t L = (uint32_t)sm.scratch[1], tl = (uint32_t)sm.scratch[2];
-        const uint32_t size = 1u << L;
-        uint8_t* scr = reinterpret_cast<uint8_t*>(sm.dt);
-        const int32_t* norm = sm.norm;
-        uint32_t* dt = sm.dt;
-        const int r = block_build_spread<NW, LMAX>(sm.norm, L, tl, scr + 3u * size, scr + 2u * size, sm.cumul,
-                                                   sm.cnt, sm.wscr, [&](uint32_t i, uint32_t s, uint32_t rk) {
-                                                       const int32_t v = norm[s];
-                                                       const uint32_t nx = (v == -1 || v < -1 ? 1u : (uint32_t)v) + rk;
-                                                       const uint32_t nb = L - ilog2u(nx);
-                                                       dt[i] = (((nx << nb) - size) & 0xFFFFu) | (s << 16) | (nb << 24);
-                                                   });
-        if (tid == 0) {
-            int rc = r;
-            bool single = false;
-            for (uint32_t q = 0; q < tl; ++q)
-                if (sm.norm[q] == (int32_t)size) single = true;
-            if (rc == FSE_OK && single && !known) rc = FSE_ERR_SINGLE_SYMBOL;
-            if (rc == FSE_OK && known && n < 2) rc = FSE_ERR_LENGTH_MISMATCH;
-            sm.scratch[3] = rc;
+    int rc;
+    int32_t hdr_bits;
+    uint32_t L;
+    if (pre) {
+        rc = info < 0 ? info : FSE_OK;
+        if (rc == FSE_OK && (!known || n < 2)) rc = FSE_ERR_LENGTH_MISMATCH;
+        hdr_bits = (info & 0xFFFF) * 8;
+        L = (uint32_t)info >> 16;
+    } else {
+        if (__builtin_amdgcn_readfirstlane(wv) == 0) {  // NormHistogram::read (lib.rs:219), scalar unit
+            uint32_t Lh = 0, tl = 0;
+            const uint32_t availw = (min(clen, PMAX) + 3u) >> 2;
+            const uint32_t r0 = lane < availw ? sm.pay[lane] : 0u;
+            const uint32_t r1 = lane + 64u < availw ? sm.pay[lane + 64u] : 0u;
+            const int hl = header_read_wave(r0, r1, clen, (uint32_t)LMAX, sm.norm, &Lh, &tl);
+            int r = hl < 0 ? hl : FSE_OK;
+            if (r == FSE_OK && ((uint32_t)hl >= clen || in[clen - 1] == 0)) r = FSE_ERR_NO_MARKER;  // lib.rs:222
+            if (lane == 0) {
+                sm.scratch[0] = hl;
+                sm.scratch[1] = (int)Lh;
+                sm.scratch[2] = (int)tl;
+                sm.scratch[3] = r;
+            }
         }
+        __syncthreads();
+        FSE_STAMP(P, 2);
+        if (sm.scratch[3] == FSE_OK) {  // DecodeTable::update (lib.rs:223, fse.rs:280-338)
+            const uint32_t Lt = (uint32_t)sm.scratch[1], tl = (uint32_t)sm.scratch[2];
+            const uint32_t size = 1u << Lt;
+            uint8_t* scr = reinterpret_cast<uint8_t*>(sm.dt);
+            const int32_t* norm = sm.norm;
+            uint32_t* dt = sm.dt;
+            const int r = block_build_spread<NW, LMAX>(sm.norm, Lt, tl, scr + 3u * size, scr + 2u * size, sm.cumul,
+                                                       sm.cnt, sm.wscr, [&](uint32_t i, uint32_t s, uint32_t rk) {
+                                                           const int32_t v = norm[s];
+                                                           const uint32_t nx = (v < 0 ? 1u : (uint32_t)v) + rk;
+                                                           const uint32_t nb = Lt - ilog2u(nx);
+                                                           dt[i] = dte_make(nb, s, (nx << nb) - size);
+                                                       });
+            if (tid == 0) {
+                int r2 = r;
+                bool single = false;
+                for (uint32_t q = 0; q < tl; ++q)
+                    if (sm.norm[q] == (int32_t)size) single = true;
+                if (r2 == FSE_OK && single && !known) r2 = FSE_ERR_SINGLE_SYMBOL;
+                if (r2 == FSE_OK && known && n < 2) r2 = FSE_ERR_LENGTH_MISMATCH;
+                sm.scratch[3] = r2;
+            }
+        }
+        __syncthreads();
+        rc = sm.scratch[3];
+        hdr_bits = sm.scratch[0] * 8;
+        L = (uint32_t)sm.scratch[1];
     }
-    __syncthreads();
     FSE_STAMP(P, 3);
-    const int rc = sm.scratch[3];
     if (rc != FSE_OK) {
         if (tid == 0) {
             P.status[gb] = rc;
@@ -729,8 +839,6 @@ __global__ __launch_bounds__(64 * NW) void decode_blocks_kernel(DecParams P) {
         }
         return;
     }
-    const int32_t hdr_bits = sm.scratch[0] * 8;
-    const uint32_t L = (uint32_t)sm.scratch[1];
     const uint32_t smask = (1u << L) - 1u;
     const uint32_t* dt = sm.dt;
     if (P.debug & 1u) {
@@ -749,16 +857,18 @@ __global__ __launch_bounds__(64 * NW) void decode_blocks_kernel(DecParams P) {
             const uint64_t e = sc[seg];
             const uint32_t p0 = seg * I;
             const uint32_t p1 = min(p0 + I, Pm);
+            const uint32_t bp = (uint32_t)e;
+            const uint32_t s0 = (uint32_t)(e >> 32) & smask, s1 = (uint32_t)(e >> 48) & smask;
             int32_t r;
-            LdsReader br;  // LDS and global instantiations stay separate (no flat loads)
-            if (in_lds) {
-                br.init(sm.pay, hdr_bits + (int32_t)(uint32_t)e);
-                r = decode_segment(br, (uint32_t)(e >> 32) & 0xFFFFu, (uint32_t)(e >> 48), p0, p1,
-                                   seg == nseg - 1u, n, Pm, out, dt, smask, hdr_bits);
+            if (bp > clen * 8u - (uint32_t)hdr_bits) {  // corrupt index: never read outside the block
+                r = FSE_ERR_BAD_ARG;
+            } else if (in_lds) {
+                r = decode_segment_lds(sm.pay, hdr_bits + (int32_t)bp, s0, s1, p0, p1, seg == nseg - 1u, n, Pm,
+                                       out, dt, hdr_bits);
             } else {
-                br.init(gwords, hdr_bits + (int32_t)(uint32_t)e);
-                r = decode_segment(br, (uint32_t)(e >> 32) & 0xFFFFu, (uint32_t)(e >> 48), p0, p1,
-                                   seg == nseg - 1u, n, Pm, out, dt, smask, hdr_bits);
+                GlobalReader br;  // LDS and global paths stay separate (no flat loads)
+                br.init(gwords, hdr_bits + (int32_t)bp);
+                r = decode_segment(br, s0, s1, p0, p1, seg == nseg - 1u, n, Pm, out, dt, smask, hdr_bits);
             }
             if (r != FSE_OK) err = r;
         }
@@ -801,43 +911,87 @@ __global__ __launch_bounds__(64 * NW) void decode_blocks_kernel(DecParams P) {
                 rec[pidx / I] = (uint64_t)(uint32_t)(br.pos - hdr_bits) | ((uint64_t)s0 << 32) |
                                 ((uint64_t)s1 << 48);
             if (known && o + 2u == n) {
-                store_byte(out, o++, cap, dt[s0 & smask] >> 16);
-                store_byte(out, o++, cap, dt[s1 & smask] >> 16);
+                store_byte(out, o++, cap, dte_sym(dt[s0 & smask]));
+                store_byte(out, o++, cap, dte_sym(dt[s1 & smask]));
                 break;
             }
             if (known && o + 1u == n) {
-                store_byte(out, o++, cap, dt[s0 & smask] >> 16);
+                store_byte(out, o++, cap, dte_sym(dt[s0 & smask]));
                 break;
             }
             const uint32_t e0 = dt[s0 & smask];
-            uint32_t nb = e0 >> 24;
+            uint32_t nb = dte_nb(e0);
             if (br.pos - (int32_t)nb < hdr_bits) {  // decode0 fails: 242-243
                 if (o + 2u > cap) { err = known ? FSE_ERR_LENGTH_MISMATCH : FSE_ERR_DST_TOO_SMALL; break; }
-                store_byte(out, o++, cap, e0 >> 16);
-                store_byte(out, o++, cap, dt[s1 & smask] >> 16);
+                store_byte(out, o++, cap, dte_sym(e0));
+                store_byte(out, o++, cap, dte_sym(dt[s1 & smask]));
                 break;
             }
-            s0 = ((e0 & 0xFFFFu) + br.pop(nb)) & 0xFFFFu;
+            s0 = dte_ns(e0) + br.pop(nb);
             br.refill();
             if (o >= cap) { err = known ? FSE_ERR_LENGTH_MISMATCH : FSE_ERR_DST_TOO_SMALL; break; }
-            store_byte(out, o++, cap, e0 >> 16);
+            store_byte(out, o++, cap, dte_sym(e0));
             const uint32_t e1 = dt[s1 & smask];
-            nb = e1 >> 24;
+            nb = dte_nb(e1);
             if (br.pos - (int32_t)nb < hdr_bits) {  // decode1 fails: 235-239
                 if (o + 2u > cap) { err = known ? FSE_ERR_LENGTH_MISMATCH : FSE_ERR_DST_TOO_SMALL; break; }
-                store_byte(out, o++, cap, e1 >> 16);
-                store_byte(out, o++, cap, dt[s0 & smask] >> 16);
+                store_byte(out, o++, cap, dte_sym(e1));
+                store_byte(out, o++, cap, dte_sym(dt[s0 & smask]));
                 break;
             }
-            s1 = ((e1 & 0xFFFFu) + br.pop(nb)) & 0xFFFFu;
+            s1 = dte_ns(e1) + br.pop(nb);
             br.refill();
             if (o >= cap) { err = known ? FSE_ERR_LENGTH_MISMATCH : FSE_ERR_DST_TOO_SMALL; break; }
-            store_byte(out, o++, cap, e1 >> 16);
+            store_byte(out, o++, cap, dte_sym(e1));
         }
     }
     if (err == FSE_OK && known && o != n) err = FSE_ERR_LENGTH_MISMATCH;
     P.status[gb] = err;
     if (P.out_len) P.out_len[gb] = err ? 0u : o;
+}
+
+// ------------------------------------------------------------------------
+// Decode tables for a batch of blocks (C3's "pre-built dtables"; also the
+// first kernel of the two-kernel decode): NormHistogram::read on the scalar
+// unit + DecodeTable (fse.rs:280-338) by one wave per block, written to HBM
+// in the decoder's entry layout.  Small LDS footprint, so many blocks are in
+// flight per CU and the serial header parse is overlapped across blocks.
+// ------------------------------------------------------------------------
+template <int LMAX>
+__global__ __launch_bounds__(64) void dtable_blocks_kernel(DtParams P) {
+    constexpr uint32_t SIZE = 1u << LMAX;
+    __shared__ int32_t norm[256];
+    __shared__ uint16_t cumul[256];
+    __shared__ uint32_t cnt[256];
+    __shared__ uint8_t sym_at[SIZE];
+    __shared__ uint8_t occ[SIZE];
+    const uint32_t lane = lane_id();
+    const uint64_t gb = blockIdx.x;
+    if (gb >= P.n_blocks) return;
+    const uint8_t* in = P.in + gb * P.slot_bytes;
+    const uint32_t clen = P.comp_len[gb];
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(in);
+    const uint32_t nw = (uint32_t)min((uint64_t)min(clen, HDR_MAX) + 3u, P.slot_bytes) >> 2;
+    const uint32_t r0 = lane < nw ? w[lane] : 0u;
+    const uint32_t r1 = lane + 64u < nw ? w[lane + 64u] : 0u;
+    for (uint32_t s = lane; s < 256u; s += WAVE) norm[s] = 0;
+    wave_sync();
+    uint32_t L = 0, tl = 0;
+    const int hl = header_read_wave(r0, r1, clen, (uint32_t)LMAX, norm, &L, &tl);
+    int rc = hl < 0 ? hl : FSE_OK;
+    if (rc == FSE_OK && ((uint32_t)hl >= clen || in[clen - 1] == 0)) rc = FSE_ERR_NO_MARKER;  // lib.rs:222
+    wave_sync();
+    if (rc == FSE_OK) {
+        const uint32_t size = 1u << L;
+        uint32_t* dt = P.dt + gb * (uint64_t)SIZE;
+        rc = wave_build_spread(norm, L, tl, sym_at, occ, cumul, cnt, [&](uint32_t i, uint32_t s, uint32_t r) {
+            const int32_t v = norm[s];
+            const uint32_t nx = (v < 0 ? 1u : (uint32_t)v) + r;
+            const uint32_t nb = L - ilog2u(nx);
+            dt[i] = dte_make(nb, s, (nx << nb) - size);
+        });
+    }
+    if (lane == 0) P.dtinfo[gb] = rc == FSE_OK ? (int32_t)((uint32_t)hl | (L << 16)) : rc;
 }
 
 // ------------------------------------------------------------------------
@@ -947,12 +1101,21 @@ hipError_t launch_encode(const EncParams& P, uint32_t lmax, hipStream_t stream) 
 }
 
 hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) {
-    constexpr uint32_t PM = 39u << 10;  // LDS stage for the compressed block (3 workgroups/CU at L<=11)
-    if (lmax <= 11) {
-        hipLaunchKernelGGL((decode_blocks_kernel<11, 4, PM>), dim3(P.n_blocks), dim3(256), 0, stream, P);
+    // LDS stage for the compressed block, sized for 3 workgroups per CU at L <= 11
+    constexpr uint32_t PM4 = 39u << 10, PM8 = 35u << 10;
+    if (P.waves == 8) {
+        if (lmax <= 11) hipLaunchKernelGGL((decode_blocks_kernel<11, 8, PM8>), dim3(P.n_blocks), dim3(512), 0, stream, P);
+        else hipLaunchKernelGGL((decode_blocks_kernel<12, 8, PM8>), dim3(P.n_blocks), dim3(512), 0, stream, P);
     } else {
-        hipLaunchKernelGGL((decode_blocks_kernel<12, 4, PM>), dim3(P.n_blocks), dim3(256), 0, stream, P);
+        if (lmax <= 11) hipLaunchKernelGGL((decode_blocks_kernel<11, 4, PM4>), dim3(P.n_blocks), dim3(256), 0, stream, P);
+        else hipLaunchKernelGGL((decode_blocks_kernel<12, 4, PM4>), dim3(P.n_blocks), dim3(256), 0, stream, P);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_dtables(const DtParams& P, uint32_t lmax, hipStream_t stream) {
+    if (lmax <= 11) hipLaunchKernelGGL((dtable_blocks_kernel<11>), dim3(P.n_blocks), dim3(64), 0, stream, P);
+    else hipLaunchKernelGGL((dtable_blocks_kernel<12>), dim3(P.n_blocks), dim3(64), 0, stream, P);
     return hipGetLastError();
 }
 

@@ -142,6 +142,33 @@ class BlockCodec:
         self.decompress_into(cb, out, status, use_sidecar)
         return out, status
 
+    def build_dtables(self, cb: dict) -> dict:
+        """Decode tables for every block of `cb` (fsehip_build_dtables): the
+        pre-built tables of decode-only workloads (C3)."""
+        t = self.torch
+        nb = self.n_blocks(cb["n_total"])
+        per = int(self.lib.fsehip_dtable_bytes(self.max_table_log))
+        tabs = {"dt": t.empty(nb * per // 4, dtype=t.int32, device=self.device),
+                "info": t.empty(nb, dtype=t.int32, device=self.device)}
+        self.build_dtables_into(cb, tabs)
+        return tabs
+
+    def build_dtables_into(self, cb: dict, tabs: dict) -> None:
+        p = self.params()
+        check(self.lib.fsehip_build_dtables(
+            C.byref(p), C.c_void_p(cb["out"].data_ptr()), self.slot_bytes, C.c_void_p(cb["comp_len"].data_ptr()),
+            self.n_blocks(cb["n_total"]), C.c_void_p(tabs["dt"].data_ptr()), C.c_void_p(tabs["info"].data_ptr()),
+            self._stream()), "fsehip_build_dtables")
+
+    def decompress_dt_into(self, cb: dict, tabs: dict, out, status) -> None:
+        """Decode with pre-built tables (needs the sidecar)."""
+        p = self.params()
+        check(self.lib.fsehip_decompress_blocks_dt(
+            C.byref(p), C.c_void_p(cb["out"].data_ptr()), self.slot_bytes, C.c_void_p(cb["comp_len"].data_ptr()),
+            C.c_void_p(cb["sidecar"].data_ptr()), C.c_void_p(tabs["dt"].data_ptr()),
+            C.c_void_p(tabs["info"].data_ptr()), C.c_void_p(out.data_ptr()), cb["n_total"],
+            C.c_void_p(status.data_ptr()), self._stream()), "fsehip_decompress_blocks_dt")
+
     def generate(self, kind: int, prob: float, seed: int, n_total: int):
         t = self.torch
         out = t.empty(n_total, dtype=t.uint8, device=self.device)

@@ -92,6 +92,22 @@ int fsehip_decompress_blocks(const fsehip_params* p, const uint8_t* d_in, uint64
                              const uint32_t* d_comp_len, const uint64_t* d_sidecar, uint8_t* d_out,
                              uint64_t n_total, int32_t* d_status, fsehip_stream_t stream);
 
+/* Decode tables, built once per block (NormHistogram::read + DecodeTable,
+ * histogram.rs:436-505, fse.rs:280-338) for decode-only workloads (C3):
+ * d_dtables holds fsehip_dtable_bytes(max_table_log) bytes per block (entry
+ * u32 = nbBits | symbol << 8 | 4*newState << 16), d_dtinfo one int32 per
+ * block (header bytes | tableLog << 16, or a negative status). */
+uint64_t fsehip_dtable_bytes(uint32_t max_table_log);
+int fsehip_build_dtables(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
+                         const uint32_t* d_comp_len, uint32_t n_blocks, uint32_t* d_dtables, int32_t* d_dtinfo,
+                         fsehip_stream_t stream);
+/* Decompress with prebuilt tables (requires the sidecar).  fsehip_decompress_blocks
+ * with a sidecar runs fsehip_build_dtables + this into a per-stream workspace. */
+int fsehip_decompress_blocks_dt(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
+                                const uint32_t* d_comp_len, const uint64_t* d_sidecar, const uint32_t* d_dtables,
+                                const int32_t* d_dtinfo, uint8_t* d_out, uint64_t n_total, int32_t* d_status,
+                                fsehip_stream_t stream);
+
 /* Serial decode that also records the sidecar index (for streams produced
  * elsewhere, e.g. by the CPU crate), so later decodes run in parallel. */
 int fsehip_build_sidecar(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,

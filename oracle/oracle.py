@@ -193,6 +193,17 @@ def header_read(data) -> tuple[Norm, int]:
     return nh, used.value
 
 
+def dtable(data):
+    """Decode table of a compressed block (NormHistogram::read +
+    DecodeTable::new): (log2, new_state[], sym[], nb[], header_bytes)."""
+    nh, used = header_read(data)
+    dt = DTable()
+    _check(lib().fo_build_dtable(C.byref(nh), C.byref(dt)))
+    size = 1 << dt.log2
+    return (dt.log2, np.ctypeslib.as_array(dt.new_state)[:size].copy(),
+            np.ctypeslib.as_array(dt.sym)[:size].copy(), np.ctypeslib.as_array(dt.nb)[:size].copy(), used)
+
+
 def checkpoints2(data, interval: int):
     a = _u8(data)
     cap = 1 << 20

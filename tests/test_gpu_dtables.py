@@ -1,0 +1,110 @@
+"""Decode tables on the GPU (fsehip_build_dtables, C3's pre-built dtables)
+against the oracle's DecodeTable (fse.rs:280-338), and the three decode
+routes (fused kernel, two-kernel default, pre-built tables) against the
+source."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+@pytest.mark.parametrize("kind,prob,log2", [(0, 0.155, 0), (2, 0.0, 12), (0, 0.77, 9), (1, 0.5, 0)])
+def test_dtables_match_oracle(torch_cuda, kind, prob, log2):
+    torch = torch_cuda
+    from entropy_coders_amd import BlockCodec
+
+    codec = BlockCodec(block_size=16384, table_log=log2, ckpt_interval=64)
+    n = 24 * 16384 + 777
+    src = codec.generate(kind, prob, 0x5EED0007, n)
+    cb = codec.compress(src)
+    tabs = codec.build_dtables(cb)
+    torch.cuda.synchronize()
+    assert int(cb["status"].abs().max()) == 0
+    info = tabs["info"].cpu().numpy()
+    per = int(codec.lib.fsehip_dtable_bytes(codec.max_table_log)) // 4
+    dt = tabs["dt"].cpu().numpy().view(np.uint32)
+    for b in range(codec.n_blocks(n)):
+        blk = codec.block_bytes(cb, b)
+        L, ns, sym, nb, used = O.dtable(blk)
+        assert info[b] >= 0, (b, info[b])
+        assert info[b] >> 16 == L and info[b] & 0xFFFF == used, b
+        e = dt[b * per: b * per + (1 << L)]
+        assert np.array_equal(e & 0xFF, nb), b
+        assert np.array_equal((e >> 8) & 0xFF, sym), b
+        assert np.array_equal(e >> 18, ns), b
+
+
+def test_decode_routes_agree(torch_cuda):
+    torch = torch_cuda
+    from entropy_coders_amd import BlockCodec
+
+    codec = BlockCodec(block_size=65536, ckpt_interval=128)
+    n = 48 * 65536 + 4321
+    src = codec.generate(0, 0.2, 0x5EED0008, n)
+    cb = codec.compress(src)
+    outs = {}
+    for name, env in (("fused4", {"FSEHIP_DEC_FUSED": "1", "FSEHIP_DEC_WAVES": "4"}),
+                      ("fused8", {"FSEHIP_DEC_FUSED": "1", "FSEHIP_DEC_WAVES": "8"}),
+                      ("two_kernel", {"FSEHIP_DEC_FUSED": "0", "FSEHIP_DEC_WAVES": "4"}),
+                      ("two_kernel8", {"FSEHIP_DEC_FUSED": "0", "FSEHIP_DEC_WAVES": "8"})):
+        old = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            out, st = codec.decompress(cb)
+            torch.cuda.synchronize()
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+        assert int(st.abs().max()) == 0, name
+        assert torch.equal(out, src), name
+        outs[name] = out
+    tabs = codec.build_dtables(cb)
+    out = torch.empty_like(src)
+    st = torch.zeros(codec.n_blocks(n), dtype=torch.int32, device=src.device)
+    codec.decompress_dt_into(cb, tabs, out, st)
+    torch.cuda.synchronize()
+    assert int(st.abs().max()) == 0 and torch.equal(out, src)
+
+
+def test_dtables_error_blocks(torch_cuda):
+    """Blocks the encoder rejected (comp_len 0) and corrupted headers report
+    the header-read status in dtinfo and in the decode status."""
+    torch = torch_cuda
+    from entropy_coders_amd import BlockCodec
+    from entropy_coders_amd._lib import STATUS
+
+    codec = BlockCodec(block_size=4096, ckpt_interval=64)
+    host = np.concatenate([O.generate(0, 0.3, 3, 0, 4096), np.zeros(4096, np.uint8),
+                           O.generate(0, 0.3, 3, 2, 4096)])
+    src = torch.from_numpy(host).cuda()
+    cb = codec.compress(src)
+    # corrupt block 2's marker byte
+    ln = int(cb["comp_len"][2])
+    cb["out"][2 * codec.slot_bytes + ln - 1] = 0
+    tabs = codec.build_dtables(cb)
+    out = torch.empty_like(src)
+    st = torch.zeros(3, dtype=torch.int32, device=src.device)
+    codec.decompress_dt_into(cb, tabs, out, st)
+    torch.cuda.synchronize()
+    info = tabs["info"].cpu().numpy()
+    stat = st.cpu().numpy()
+    assert info[0] >= 0 and stat[0] == 0
+    assert STATUS[int(info[1])] == "EMPTY" and stat[1] == info[1]
+    assert STATUS[int(info[2])] == "NO_MARKER" and stat[2] == info[2]
+    assert np.array_equal(out[:4096].cpu().numpy(), host[:4096])
