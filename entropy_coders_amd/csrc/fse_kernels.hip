@@ -16,6 +16,8 @@
 // Decode (one 64-lane workgroup per block): header parse, decode table in
 //   LDS, then each lane decodes the checkpoint segments assigned to it.
 //   Without a sidecar one lane decodes the block serially (reference mode).
+#include <type_traits>
+
 #include "fse_device.hpp"
 #include "fse_kernels.h"
 
@@ -630,53 +632,124 @@ __device__ __forceinline__ uint32_t lds_bits32(const uint32_t* pay, int32_t pos)
     return __builtin_amdgcn_alignbit(wp[1], wp[0], (uint32_t)pos);
 }
 
-// The same segment decode for a block staged in LDS, with absolute bit
-// addressing and no reader state: per pair, pos -= nb0 + nb1 (byte sum of
-// the two entries), one 32-bit window at pos, then v1 = low nb1 bits and
-// v0 = the nb0 bits above (stack order: decoder 0 pops first), and the next
-// states' LDS offsets.  32 pairs = one whole 64-byte segment per lane are
-// stored back to back (full HBM write bursts).  `a0`/`a1` are LDS byte
-// offsets of the current states' entries.
-__device__ __forceinline__ int32_t decode_segment_lds(const uint32_t* pay, int32_t pos, uint32_t s0, uint32_t s1,
-                                                      uint32_t p0, uint32_t p1, bool last, uint32_t n, uint32_t Pm,
-                                                      uint8_t* __restrict__ out, const uint32_t* dt,
-                                                      int32_t hdr_bits) {
-    const uint8_t* dtb = reinterpret_cast<const uint8_t*>(dt);
-    uint32_t a0 = s0 << 2, a1 = s1 << 2;
-    auto pair = [&]() -> uint32_t {
-        const uint32_t e0 = *reinterpret_cast<const uint32_t*>(dtb + a0);
-        const uint32_t e1 = *reinterpret_cast<const uint32_t*>(dtb + a1);
-        pos -= (int32_t)((e0 + e1) & 0xFFu);
-        const uint32_t x = lds_bits32(pay, pos);
+// Padded LDS image of a block (VAR 3): source word w lives at LDS word
+// w + w/32, and the dword after each 32-word row repeats the next row's
+// first word, so words w and w+1 are always adjacent (one ds_read2).  Lanes
+// that walk equal-size segments in lockstep then land on different banks:
+// a segment stride of S words puts lane l at bank ~(S * 33/32 * l) mod 32
+// instead of (S * l) mod 32, which for S ~ 32 (C2) collapsed onto a handful
+// of banks.
+__device__ __forceinline__ uint32_t pad_word(uint32_t w) { return w + (w >> 5); }
+__device__ __forceinline__ uint32_t lds_bits32_pad(const uint32_t* pay, int32_t pos) {
+    const uint32_t* wp = pay + pad_word((uint32_t)pos >> 5);
+    return __builtin_amdgcn_alignbit(wp[1], wp[0], (uint32_t)pos);
+}
+template <int VAR>
+__device__ __forceinline__ uint32_t lds_bits(const uint32_t* pay, int32_t pos) {
+    return VAR == 3 ? lds_bits32_pad(pay, pos) : lds_bits32(pay, pos);
+}
+
+// Segment decode for a block staged in LDS.  One LdsChain = one segment's
+// decoder pair (two tANS states + the shared bit position).  Per pair:
+// pos -= nb0 + nb1 (byte sum of the two entries), the pair's bits at pos,
+// v1 = low nb1 bits and v0 = the nb0 bits above (stack order: decoder 0
+// pops first), and the next states' LDS offsets a0/a1 (4 * state).
+//   VAR 0: one ds_read2 of the two words at pos per pair;
+//   VAR 1: the same window fetched from pos_prev - 24 alongside the table
+//          reads (one LDS latency on the chain instead of two);
+//   VAR 2: a per-lane 64-bit window over words (k, k+1), B = 32k, holding
+//          >= 32 bits below pos at each pair start; refills are exec-masked
+//          to the lanes that need one, the next word prefetched a refill
+//          ahead.  Lanes walk equal-size segments in lockstep, so unmasked
+//          per-pair payload reads pile onto a few banks.
+template <int VAR>
+struct LdsChain {
+    int32_t pos, B;
+    uint32_t wlo, whi, wnx, a0, a1;
+    __device__ __forceinline__ void init(const uint32_t* pay, int32_t p, uint32_t s0, uint32_t s1) {
+        pos = p;
+        a0 = s0 << 2;
+        a1 = s1 << 2;
+        B = 0;
+        wlo = whi = wnx = 0;
+        if (VAR == 2) {
+            const int32_t k = max((p >> 5) - 1, 0);
+            B = k << 5;
+            wlo = pay[k];
+            whi = pay[k + 1];
+            wnx = pay[max(k - 1, 0)];
+        }
+    }
+    __device__ __forceinline__ uint32_t pair(const uint32_t* pay, const uint8_t* dtb) {
+        uint32_t x, e0, e1;
+        if (VAR == 2) {
+            e0 = *reinterpret_cast<const uint32_t*>(dtb + a0);
+            e1 = *reinterpret_cast<const uint32_t*>(dtb + a1);
+            pos -= (int32_t)((e0 + e1) & 0xFFu);
+            x = (uint32_t)((((uint64_t)whi << 32) | wlo) >> (uint32_t)(pos - B));
+            if (pos < B + 32) {
+                B -= 32;
+                whi = wlo;
+                wlo = wnx;
+                wnx = pay[max((B >> 5) - 1, 0)];
+            }
+        } else if (VAR == 1) {
+            const int32_t lo = max(pos - 24, 0);
+            const uint32_t* wp = pay + ((uint32_t)lo >> 5);
+            const uint32_t w0 = wp[0], w1 = wp[1];
+            const uint32_t base = (uint32_t)lo & ~31u;
+            e0 = *reinterpret_cast<const uint32_t*>(dtb + a0);
+            e1 = *reinterpret_cast<const uint32_t*>(dtb + a1);
+            pos -= (int32_t)((e0 + e1) & 0xFFu);
+            x = (uint32_t)((((uint64_t)w1 << 32) | w0) >> ((uint32_t)pos - base));
+        } else {
+            e0 = *reinterpret_cast<const uint32_t*>(dtb + a0);
+            e1 = *reinterpret_cast<const uint32_t*>(dtb + a1);
+            pos -= (int32_t)((e0 + e1) & 0xFFu);
+            x = lds_bits<VAR>(pay, pos);
+        }
         const uint32_t v1 = __builtin_amdgcn_ubfe(x, 0u, e1);
         const uint32_t v0 = __builtin_amdgcn_ubfe(x, e1, e0);
         a0 = (e0 >> 16) + (v0 << 2);
         a1 = (e1 >> 16) + (v1 << 2);
         return __builtin_amdgcn_perm(e1, e0, 0x0c0c0501u);  // sym0 | sym1 << 8
-    };
-    uint32_t p = p0;
+    }
+};
+
+// 32 pairs = one whole 64-byte segment of output per lane, stored back to
+// back (full HBM write bursts instead of masked partial ones).
+__device__ __forceinline__ void store_group(uint8_t* __restrict__ dst, const uint32_t* w) {
+    uint4* o4 = reinterpret_cast<uint4*>(dst);
+#pragma unroll
+    for (uint32_t q = 0; q < DEC_GROUP / 8u; ++q) o4[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+}
+
+// Pairs [p, p1) of one chain, then (when `last`) the reference termination
+// in container mode (the oracle's decompress2_impl; lib.rs:227-244).
+template <int VAR>
+__device__ __forceinline__ int32_t run_chain(LdsChain<VAR>& c, const uint32_t* pay, const uint8_t* dtb, uint32_t p,
+                                             uint32_t p1, bool last, uint32_t n, uint32_t Pm,
+                                             uint8_t* __restrict__ out, int32_t hdr_bits) {
     for (; p + DEC_GROUP <= p1; p += DEC_GROUP) {
         uint32_t w[DEC_GROUP / 2u];
 #pragma unroll
         for (uint32_t j = 0; j < DEC_GROUP; j += 2u) {
-            const uint32_t lo = pair();
-            const uint32_t hi = pair();
+            const uint32_t lo = c.pair(pay, dtb);
+            const uint32_t hi = c.pair(pay, dtb);
             w[j >> 1] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);  // lo.b0 lo.b1 hi.b0 hi.b1
         }
-        uint4* o4 = reinterpret_cast<uint4*>(out + 2u * p);
-#pragma unroll
-        for (uint32_t q = 0; q < DEC_GROUP / 8u; ++q)
-            o4[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+        store_group(out + 2u * p, w);
     }
     for (; p < p1; ++p) {
-        const uint32_t pr = pair();
+        const uint32_t pr = c.pair(pay, dtb);
         out[2u * p] = (uint8_t)pr;
         out[2u * p + 1u] = (uint8_t)(pr >> 8);
     }
     if (!last) return FSE_OK;
-    // container-mode termination (lib.rs:227-244 with the raw length known)
     auto ent = [&](uint32_t a) { return *reinterpret_cast<const uint32_t*>(dtb + a); };
     uint32_t o = 2u * Pm;
+    int32_t pos = c.pos;
+    uint32_t a0 = c.a0, a1 = c.a1;
     for (;;) {
         if (o + 2u == n) {
             out[o++] = (uint8_t)dte_sym(ent(a0));
@@ -695,7 +768,7 @@ __device__ __forceinline__ int32_t decode_segment_lds(const uint32_t* pay, int32
             break;
         }
         pos -= (int32_t)nb;
-        a0 = (e0 >> 16) + (__builtin_amdgcn_ubfe(lds_bits32(pay, pos), 0u, nb) << 2);
+        a0 = (e0 >> 16) + (__builtin_amdgcn_ubfe(lds_bits<VAR>(pay, pos), 0u, nb) << 2);
         out[o++] = (uint8_t)dte_sym(e0);
         const uint32_t e1 = ent(a1);
         nb = dte_nb(e1);
@@ -705,7 +778,7 @@ __device__ __forceinline__ int32_t decode_segment_lds(const uint32_t* pay, int32
             break;
         }
         pos -= (int32_t)nb;
-        a1 = (e1 >> 16) + (__builtin_amdgcn_ubfe(lds_bits32(pay, pos), 0u, nb) << 2);
+        a1 = (e1 >> 16) + (__builtin_amdgcn_ubfe(lds_bits<VAR>(pay, pos), 0u, nb) << 2);
         out[o++] = (uint8_t)dte_sym(e1);
     }
     return o == n ? FSE_OK : FSE_ERR_LENGTH_MISMATCH;
@@ -746,21 +819,36 @@ __global__ __launch_bounds__(64 * NW) void decode_blocks_kernel(DecParams P) {
     const uint32_t n = known ? (uint32_t)min((uint64_t)P.block_size, P.n_total - ooff) : 0u;
     const uint32_t cap = known ? n : P.out_cap;
     uint8_t* out = P.out + ooff;
-    const bool in_lds = clen <= PMAX;
     // prebuilt decode tables (dtable_blocks_kernel / C3): no header parse, no table build
     const bool pre = P.dt != nullptr;
     const int32_t info = pre ? P.dtinfo[gb] : 0;
+    const bool padded = pre && P.variant == 3;
+    const uint32_t nwords = (clen + 3u) >> 2;
+    const bool in_lds = padded ? (pad_word(nwords) + 2u) * 4u <= PMAX : clen <= PMAX;
     FSE_STAMP(P, 0);
 
     {  // stage the block (or at least its header) in LDS, plus a prebuilt table
-        const uint32_t ncopy = in_lds ? clen : min(clen, (uint32_t)min((uint64_t)HDR_MAX, P.slot_bytes));
-        const uint32_t nvec = (pre && info < 0) ? 0u : (ncopy + 15u) >> 4;
-        const uint4* src4 = reinterpret_cast<const uint4*>(in);
-        uint4* dst4 = reinterpret_cast<uint4*>(sm.pay);
-        // LDS-DMA: each wave-instruction moves 1 KiB, lane-linear in LDS
-        for (uint32_t i = wv * 64u; i < nvec; i += 64u * NW) {
-            if (i + lane < nvec)
-                __builtin_amdgcn_global_load_lds(src4 + i + lane, dst4 + i, 16, 0, 0);
+        if (padded && in_lds && info >= 0) {
+            // dword LDS-DMA: LDS word d <- source word d - d/33 (the 33rd
+            // dword of each row repeats the next row's first word)
+            const uint32_t nd = pad_word(nwords) + 2u;
+            const uint32_t wmax = (uint32_t)min((uint64_t)nwords + 1u, P.slot_bytes / 4u) - 1u;
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(in);
+            for (uint32_t i = wv * 64u; i < nd; i += 64u * NW) {
+                const uint32_t d = i + lane;
+                const uint32_t w = min(d - d / 33u, wmax);
+                if (d < nd) __builtin_amdgcn_global_load_lds(src + w, sm.pay + i, 4, 0, 0);
+            }
+        } else {
+            const uint32_t ncopy = in_lds ? clen : min(clen, (uint32_t)min((uint64_t)HDR_MAX, P.slot_bytes));
+            const uint32_t nvec = (pre && info < 0) ? 0u : (ncopy + 15u) >> 4;
+            const uint4* src4 = reinterpret_cast<const uint4*>(in);
+            uint4* dst4 = reinterpret_cast<uint4*>(sm.pay);
+            // LDS-DMA: each wave-instruction moves 1 KiB, lane-linear in LDS
+            for (uint32_t i = wv * 64u; i < nvec; i += 64u * NW) {
+                if (i + lane < nvec)
+                    __builtin_amdgcn_global_load_lds(src4 + i + lane, dst4 + i, 16, 0, 0);
+            }
         }
         if (pre && info >= 0) {
             const uint32_t dvec = 1u << ((uint32_t)info >> 16) >> 2;  // 4 << L bytes
@@ -853,24 +941,38 @@ __global__ __launch_bounds__(64 * NW) void decode_blocks_kernel(DecParams P) {
         const uint32_t nseg = Pm / I + 1u;
         const uint64_t* sc = P.sidecar + gb * P.ckpt_per_block;
         int32_t err = FSE_OK;
-        for (uint32_t seg = tid; seg < nseg; seg += 64u * NW) {
-            const uint64_t e = sc[seg];
-            const uint32_t p0 = seg * I;
-            const uint32_t p1 = min(p0 + I, Pm);
-            const uint32_t bp = (uint32_t)e;
-            const uint32_t s0 = (uint32_t)(e >> 32) & smask, s1 = (uint32_t)(e >> 48) & smask;
-            int32_t r;
-            if (bp > clen * 8u - (uint32_t)hdr_bits) {  // corrupt index: never read outside the block
-                r = FSE_ERR_BAD_ARG;
-            } else if (in_lds) {
-                r = decode_segment_lds(sm.pay, hdr_bits + (int32_t)bp, s0, s1, p0, p1, seg == nseg - 1u, n, Pm,
-                                       out, dt, hdr_bits);
-            } else {
-                GlobalReader br;  // LDS and global paths stay separate (no flat loads)
-                br.init(gwords, hdr_bits + (int32_t)bp);
-                r = decode_segment(br, s0, s1, p0, p1, seg == nseg - 1u, n, Pm, out, dt, smask, hdr_bits);
+        const uint32_t maxbp = clen * 8u - (uint32_t)hdr_bits;
+        const uint8_t* dtb = reinterpret_cast<const uint8_t*>(dt);
+        constexpr uint32_t NT = 64u * NW;
+        auto seg_ok = [&](uint64_t e) { return (uint32_t)e <= maxbp; };  // corrupt index: never read outside
+        {
+            for (uint32_t seg = tid; seg < nseg; seg += NT) {
+                const uint64_t e = sc[seg];
+                const uint32_t p0 = seg * I;
+                const uint32_t p1 = min(p0 + I, Pm);
+                const uint32_t bp = (uint32_t)e;
+                const uint32_t s0 = (uint32_t)(e >> 32) & smask, s1 = (uint32_t)(e >> 48) & smask;
+                int32_t r;
+                if (!seg_ok(e)) {
+                    r = FSE_ERR_BAD_ARG;
+                } else if (in_lds) {
+                    const bool lastseg = seg == nseg - 1u;
+                    if (padded) {
+                        LdsChain<3> c;
+                        c.init(sm.pay, hdr_bits + (int32_t)bp, s0, s1);
+                        r = run_chain(c, sm.pay, dtb, p0, p1, lastseg, n, Pm, out, hdr_bits);
+                    } else {
+                        LdsChain<2> c;
+                        c.init(sm.pay, hdr_bits + (int32_t)bp, s0, s1);
+                        r = run_chain(c, sm.pay, dtb, p0, p1, lastseg, n, Pm, out, hdr_bits);
+                    }
+                } else {
+                    GlobalReader br;  // LDS and global paths stay separate (no flat loads)
+                    br.init(gwords, hdr_bits + (int32_t)bp);
+                    r = decode_segment(br, s0, s1, p0, p1, seg == nseg - 1u, n, Pm, out, dt, smask, hdr_bits);
+                }
+                if (r != FSE_OK) err = r;
             }
-            if (r != FSE_OK) err = r;
         }
         err = -(int32_t)wave_max((uint32_t)(-err));
         if (lane == 0) sm.err[wv] = err;
@@ -948,6 +1050,115 @@ __global__ __launch_bounds__(64 * NW) void decode_blocks_kernel(DecParams P) {
     if (err == FSE_OK && known && o != n) err = FSE_ERR_LENGTH_MISMATCH;
     P.status[gb] = err;
     if (P.out_len) P.out_len[gb] = err ? 0u : o;
+}
+
+// ------------------------------------------------------------------------
+// Segment decode with prebuilt tables (the default sidecar decode and C3):
+// no header parse, no table build, no serial path, so the kernel is small
+// and its LDS is the block image plus the table.  VAR 3 stages the block as
+// the padded image (pad_word), VAR 2 linearly with per-lane windows.
+// ------------------------------------------------------------------------
+template <int LMAX, uint32_t PMAX>
+struct PreSmem {
+    uint32_t pay[PMAX / 4];
+    uint32_t dt[1u << LMAX];
+    int err[16];
+};
+
+template <int LMAX, int NW, uint32_t PMAX, int VAR>
+__global__ __launch_bounds__(64 * NW) void decode_pre_kernel(DecParams P) {
+    __shared__ PreSmem<LMAX, PMAX> sm;
+    constexpr uint32_t NT = 64u * NW;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    const uint64_t gb = blockIdx.x;
+    if (gb >= P.n_blocks) return;
+    const uint8_t* in = P.in + gb * P.slot_bytes;
+    const uint32_t clen = P.comp_len[gb];
+    const uint64_t ooff = gb * (uint64_t)P.block_size;
+    const uint32_t n = (uint32_t)min((uint64_t)P.block_size, P.n_total - ooff);
+    uint8_t* out = P.out + ooff;
+    const int32_t info = P.dtinfo[gb];
+    const uint32_t nwords = (clen + 3u) >> 2;
+    const bool in_lds = VAR == 3 ? (pad_word(nwords) + 2u) * 4u <= PMAX : clen <= PMAX;
+    FSE_STAMP(P, 0);
+    if (info < 0 || n < 2) {
+        if (tid == 0) P.status[gb] = info < 0 ? info : FSE_ERR_LENGTH_MISMATCH;
+        return;
+    }
+    const int32_t hdr_bits = (info & 0xFFFF) * 8;
+    const uint32_t L = (uint32_t)info >> 16;
+    {  // stage the block image and the table
+        if (in_lds) {
+            if (VAR == 3) {
+                // dword LDS-DMA: LDS word d <- source word d - d/33
+                const uint32_t nd = pad_word(nwords) + 2u;
+                const uint32_t wmax = (uint32_t)min((uint64_t)nwords + 1u, P.slot_bytes / 4u) - 1u;
+                const uint32_t* src = reinterpret_cast<const uint32_t*>(in);
+                for (uint32_t i = wv * 64u; i < nd; i += NT) {
+                    const uint32_t d = i + lane;
+                    const uint32_t w = min(d - d / 33u, wmax);
+                    if (d < nd) __builtin_amdgcn_global_load_lds(src + w, sm.pay + i, 4, 0, 0);
+                }
+            } else {
+                const uint32_t nvec = (clen + 15u) >> 4;
+                const uint4* src4 = reinterpret_cast<const uint4*>(in);
+                uint4* dst4 = reinterpret_cast<uint4*>(sm.pay);
+                for (uint32_t i = wv * 64u; i < nvec; i += NT)
+                    if (i + lane < nvec) __builtin_amdgcn_global_load_lds(src4 + i + lane, dst4 + i, 16, 0, 0);
+            }
+        }
+        const uint32_t dvec = 1u << L >> 2;  // 4 << L bytes
+        const uint4* t4 = reinterpret_cast<const uint4*>(P.dt + gb * (uint64_t)(1u << LMAX));
+        uint4* d4 = reinterpret_cast<uint4*>(sm.dt);
+        for (uint32_t i = wv * 64u; i < dvec; i += NT)
+            if (i + lane < dvec) __builtin_amdgcn_global_load_lds(t4 + i + lane, d4 + i, 16, 0, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    FSE_STAMP(P, 3);
+    if (P.debug & 1u) {
+        if (tid == 0) P.status[gb] = FSE_OK;
+        return;
+    }
+    const uint32_t smask = (1u << L) - 1u;
+    const uint32_t Pm = (n & 1u) ? (n - 3u) / 2u : n / 2u - 1u;
+    const uint32_t I = P.ckpt_interval;
+    const uint32_t nseg = Pm / I + 1u;
+    const uint64_t* sc = P.sidecar + gb * P.ckpt_per_block;
+    const uint32_t maxbp = clen * 8u - (uint32_t)hdr_bits;
+    const uint8_t* dtb = reinterpret_cast<const uint8_t*>(sm.dt);
+    int32_t err = FSE_OK;
+    for (uint32_t seg = tid; seg < nseg; seg += NT) {
+        const uint64_t e = sc[seg];
+        const uint32_t p0 = seg * I, p1 = min(p0 + I, Pm);
+        const uint32_t bp = (uint32_t)e;
+        const uint32_t s0 = (uint32_t)(e >> 32) & smask, s1 = (uint32_t)(e >> 48) & smask;
+        const bool lastseg = seg == nseg - 1u;
+        int32_t r;
+        if (bp > maxbp) {  // corrupt index: never read outside the block
+            r = FSE_ERR_BAD_ARG;
+        } else if (in_lds) {
+            LdsChain<VAR> c;
+            c.init(sm.pay, hdr_bits + (int32_t)bp, s0, s1);
+            r = run_chain(c, sm.pay, dtb, p0, p1, lastseg, n, Pm, out, hdr_bits);
+        } else {
+            GlobalReader br;
+            br.init(reinterpret_cast<const uint32_t*>(in), hdr_bits + (int32_t)bp);
+            r = decode_segment(br, s0, s1, p0, p1, lastseg, n, Pm, out, sm.dt, smask, hdr_bits);
+        }
+        if (r != FSE_OK) err = r;
+    }
+    err = -(int32_t)wave_max((uint32_t)(-err));
+    if (lane == 0) sm.err[wv] = err;
+    __syncthreads();
+    FSE_STAMP(P, 4);
+    if (tid == 0) {
+        int32_t e2 = FSE_OK;
+        for (int w = 0; w < NW; ++w)
+            if (sm.err[w] != FSE_OK) e2 = sm.err[w];
+        P.status[gb] = e2;
+        if (P.out_len) P.out_len[gb] = e2 ? 0u : n;
+    }
 }
 
 // ------------------------------------------------------------------------
@@ -1103,12 +1314,35 @@ hipError_t launch_encode(const EncParams& P, uint32_t lmax, hipStream_t stream) 
 hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) {
     // LDS stage for the compressed block, sized for 3 workgroups per CU at L <= 11
     constexpr uint32_t PM4 = 39u << 10, PM8 = 35u << 10;
+    const dim3 g(P.n_blocks);
+    if (P.dt) {  // prebuilt tables: lean kernel; LDS = image + table (44 KB image -> 3 WG/CU)
+        constexpr uint32_t PP = 44u << 10;
+        const bool pad = P.variant == 3;
+        if (P.waves == 8) {
+            if (lmax <= 11) {
+                if (pad) hipLaunchKernelGGL((decode_pre_kernel<11, 8, PP, 3>), g, dim3(512), 0, stream, P);
+                else hipLaunchKernelGGL((decode_pre_kernel<11, 8, PP, 2>), g, dim3(512), 0, stream, P);
+            } else {
+                if (pad) hipLaunchKernelGGL((decode_pre_kernel<12, 8, PP - 8192, 3>), g, dim3(512), 0, stream, P);
+                else hipLaunchKernelGGL((decode_pre_kernel<12, 8, PP - 8192, 2>), g, dim3(512), 0, stream, P);
+            }
+        } else {
+            if (lmax <= 11) {
+                if (pad) hipLaunchKernelGGL((decode_pre_kernel<11, 4, PP, 3>), g, dim3(256), 0, stream, P);
+                else hipLaunchKernelGGL((decode_pre_kernel<11, 4, PP, 2>), g, dim3(256), 0, stream, P);
+            } else {
+                if (pad) hipLaunchKernelGGL((decode_pre_kernel<12, 4, PP - 8192, 3>), g, dim3(256), 0, stream, P);
+                else hipLaunchKernelGGL((decode_pre_kernel<12, 4, PP - 8192, 2>), g, dim3(256), 0, stream, P);
+            }
+        }
+        return hipGetLastError();
+    }
     if (P.waves == 8) {
-        if (lmax <= 11) hipLaunchKernelGGL((decode_blocks_kernel<11, 8, PM8>), dim3(P.n_blocks), dim3(512), 0, stream, P);
-        else hipLaunchKernelGGL((decode_blocks_kernel<12, 8, PM8>), dim3(P.n_blocks), dim3(512), 0, stream, P);
+        if (lmax <= 11) hipLaunchKernelGGL((decode_blocks_kernel<11, 8, PM8>), g, dim3(512), 0, stream, P);
+        else hipLaunchKernelGGL((decode_blocks_kernel<12, 8, PM8>), g, dim3(512), 0, stream, P);
     } else {
-        if (lmax <= 11) hipLaunchKernelGGL((decode_blocks_kernel<11, 4, PM4>), dim3(P.n_blocks), dim3(256), 0, stream, P);
-        else hipLaunchKernelGGL((decode_blocks_kernel<12, 4, PM4>), dim3(P.n_blocks), dim3(256), 0, stream, P);
+        if (lmax <= 11) hipLaunchKernelGGL((decode_blocks_kernel<11, 4, PM4>), g, dim3(256), 0, stream, P);
+        else hipLaunchKernelGGL((decode_blocks_kernel<12, 4, PM4>), g, dim3(256), 0, stream, P);
     }
     return hipGetLastError();
 }

@@ -56,10 +56,12 @@ def test_decode_routes_agree(torch_cuda):
     src = codec.generate(0, 0.2, 0x5EED0008, n)
     cb = codec.compress(src)
     outs = {}
-    for name, env in (("fused4", {"FSEHIP_DEC_FUSED": "1", "FSEHIP_DEC_WAVES": "4"}),
-                      ("fused8", {"FSEHIP_DEC_FUSED": "1", "FSEHIP_DEC_WAVES": "8"}),
-                      ("two_kernel", {"FSEHIP_DEC_FUSED": "0", "FSEHIP_DEC_WAVES": "4"}),
-                      ("two_kernel8", {"FSEHIP_DEC_FUSED": "0", "FSEHIP_DEC_WAVES": "8"})):
+    for name, env in (("fused4", {"FSEHIP_DEC_FUSED": "1", "FSEHIP_DEC_WAVES": "4", "FSEHIP_DEC_VAR": "2"}),
+                      ("fused8", {"FSEHIP_DEC_FUSED": "1", "FSEHIP_DEC_WAVES": "8", "FSEHIP_DEC_VAR": "2"}),
+                      ("two_kernel", {"FSEHIP_DEC_FUSED": "0", "FSEHIP_DEC_WAVES": "4", "FSEHIP_DEC_VAR": "2"}),
+                      ("two_kernel8", {"FSEHIP_DEC_FUSED": "0", "FSEHIP_DEC_WAVES": "8", "FSEHIP_DEC_VAR": "2"}),
+                      ("padded4", {"FSEHIP_DEC_FUSED": "0", "FSEHIP_DEC_WAVES": "4", "FSEHIP_DEC_VAR": "3"}),
+                      ("padded8", {"FSEHIP_DEC_FUSED": "0", "FSEHIP_DEC_WAVES": "8", "FSEHIP_DEC_VAR": "3"})):
         old = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
         try:

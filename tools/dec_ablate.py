@@ -22,8 +22,10 @@ def main():
         cb = codec.compress(src)
         out = torch.empty(n, dtype=torch.uint8, device="cuda")
         st = torch.zeros(codec.n_blocks(n), dtype=torch.int32, device="cuda")
-        for waves in (4, 8):
+        for waves, var, dual in ((4, 2, 0), (4, 3, 0), (8, 2, 0), (8, 3, 0)):
             os.environ["FSEHIP_DEC_WAVES"] = str(waves)
+            os.environ["FSEHIP_DEC_VAR"] = str(var)
+            os.environ["FSEHIP_DEC_DUAL"] = str(dual)
             os.environ["FSEHIP_DEBUG"] = str(1 << 4)
             t_ht = timeit(lambda: codec.decompress_into(cb, out, st))
             os.environ["FSEHIP_DEBUG"] = "0"
@@ -31,7 +33,7 @@ def main():
             t = timeit(lambda: codec.decompress_into(cb, out, st))
             torch.cuda.synchronize()
             ok = bool(torch.equal(out, src)) and int(st.abs().max()) == 0
-            print(f"ckpt={ckpt:4d} waves={waves}  header+table {t_ht:.4f} ms  full {t:.4f} ms  ok={ok}", flush=True)
+            print(f"ckpt={ckpt:4d} waves={waves} var={var} dual={dual}  header+table {t_ht:.4f} ms  full {t:.4f} ms  ok={ok}", flush=True)
         del cb, src, out
 
 
