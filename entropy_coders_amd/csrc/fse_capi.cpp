@@ -58,9 +58,17 @@ struct Stamps {
                 if (a && b && b >= a) { acc[k] += (double)(b - a); cnt[k]++; }
             }
         fprintf(stderr, "[stamps] %s:", what);
-        for (int k = 1; k < fsehip::kStamps; ++k)
+        for (int k = 1; k < fsehip::kStamps - 1; ++k)
             if (cnt[k]) fprintf(stderr, " %d:%.0f", k, acc[k] / cnt[k]);
         fprintf(stderr, " (mean cycles per workgroup between stamps k-1 and k)\n");
+        // slot kStamps-1: kernel-defined counters (low / high 32 bits), averaged
+        double lo = 0, hi = 0;
+        for (size_t g = 0; g < groups; ++g) {
+            const uint64_t v = h[g * fsehip::kStamps + fsehip::kStamps - 1];
+            lo += (double)(v & 0xFFFFFFFFu);
+            hi += (double)(v >> 32);
+        }
+        fprintf(stderr, "[stamps] %s counters: lo %.3f hi %.3f (mean per workgroup)\n", what, lo / groups, hi / groups);
     }
 };
 Stamps g_stamps_enc, g_stamps_dec;

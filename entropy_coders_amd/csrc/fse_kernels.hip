@@ -64,9 +64,11 @@ struct Emit {
     uint32_t word;
     uint32_t w0;        // first word index of the lane
     uint32_t head_val;  // lane's bits of word w0 once it was stored
+    uint32_t wlim;      // words in the slot: stores never leave it
     uint32_t* gw;
-    __device__ __forceinline__ void start(uint32_t* g, uint32_t off) {
+    __device__ __forceinline__ void start(uint32_t* g, uint32_t off, uint32_t lim = 0xFFFFFFFFu) {
         gw = g;
+        wlim = lim;
         acc = 0;
         nacc = off & 31u;
         word = off >> 5;
@@ -80,7 +82,7 @@ struct Emit {
     __device__ __forceinline__ void flush() {
         const bool f = nacc >= 32u;
         const uint32_t val = (uint32_t)acc;
-        if (f) gw[word] = val;
+        if (f && word < wlim) gw[word] = val;
         head_val = (f && word == w0) ? val : head_val;
         acc = f ? (acc >> 32) : acc;
         nacc -= f ? 32u : 0u;
@@ -97,7 +99,30 @@ struct Ckpt {
     uint32_t L;
 };
 
-enum { PASS_SPEC = 0, PASS_COUNT = 1, PASS_EMIT = 2 };
+enum { PASS_SPEC = 0, PASS_COUNT = 1, PASS_EMIT = 2, PASS_REPAIR = 3 };
+
+// Trajectory of a count pass, for convergence-based repair: the state pair
+// and running bit count after every ckc-th chunk (at most 8 slots per lane,
+// slot 0 = the lane's end).  A repair re-encodes from the corrected start
+// state only until it meets the recorded trajectory: from there on states
+// and bits are identical, so the lane's total follows from the record and
+// its end state (its neighbour's start) is unchanged.
+// Slots hold {x0 | x1 << 16, bits still to come after the slot}: a pass
+// writes its running count there, and track_fixup turns the slots it wrote
+// into remaining counts once the pass total is known, so every slot stays
+// consistent with the lane's current trajectory.
+struct Track {
+    uint2* cp;        // this lane's slots (LDS)
+    uint32_t ckc;     // chunks per slot
+    bool done;        // REPAIR: met the recorded trajectory
+    uint32_t jstar;   // REPAIR: the slot where it did (slots above it were rewritten)
+};
+
+// After a pass with total `total`: slots above `jlo` (exclusive) hold
+// running counts; make them remaining counts.
+__device__ __forceinline__ void track_fixup(Track& tr, uint32_t nslot, int32_t jlo, uint32_t total) {
+    for (int32_t j = (int32_t)nslot - 1; j > jlo; --j) tr.cp[j].y = total - tr.cp[j].y;
+}
 
 struct EncState {
     uint32_t x0, x1, bits;
@@ -135,7 +160,7 @@ __device__ __forceinline__ void enc_chunk(const uint4& q, uint32_t c8, uint32_t 
         x1 = *reinterpret_cast<const uint16_t*>(T.st + ((x1 >> nb1) << 1) + (int32_t)t1[j].y);
         const uint32_t nb0 = (t0[j].x + x0) >> 16;
         x0 = *reinterpret_cast<const uint16_t*>(T.st + ((x0 >> nb0) << 1) + (int32_t)t0[j].y);
-        if (MODE == PASS_COUNT) bits += nb1 + nb0;
+        if (MODE == PASS_COUNT || MODE == PASS_REPAIR) bits += nb1 + nb0;
         if (MODE == PASS_EMIT) {
             const uint32_t pairbits = (v1 & ((1u << nb1) - 1u)) | ((v0 & ((1u << nb0) - 1u)) << nb1);
             em.put(pairbits, nb1 + nb0);
@@ -158,39 +183,70 @@ __device__ __forceinline__ void ckpt_record(const Ckpt& ck, uint32_t p, uint32_t
 // segment); the partial topmost chunk is peeled and loaded byte-wise.
 template <int MODE>
 __device__ __forceinline__ EncState enc_range(const uint8_t* __restrict__ blk, uint32_t n, uint32_t pa, uint32_t pb,
-                                              EncState st, const EncTab& T, Emit& em, const Ckpt& ck) {
+                                              EncState st, const EncTab& T, Emit& em, const Ckpt& ck, Track& tr) {
+    constexpr bool TRACK = MODE == PASS_COUNT || MODE == PASS_REPAIR;
     uint32_t x0 = st.x0, x1 = st.x1, bits = st.bits;
     if (pb <= pa) return st;
     const uint4* v = reinterpret_cast<const uint4*>(blk);
     int32_t c_hi = (int32_t)((pb - 1u) >> 3);
     const int32_t c_lo = (int32_t)(pa >> 3);
+    // checkpoint after chunk c when (c - c_lo) % ckc == 0; slot (c - c_lo) / ckc
+    uint32_t rem = 0, slot = 0;
+    if (TRACK) {
+        rem = (uint32_t)(c_hi - c_lo) % tr.ckc;
+        slot = (uint32_t)(c_hi - c_lo) / tr.ckc;
+    }
+    auto track = [&]() {
+        if (rem == 0u) {
+            const uint32_t sv = x0 | (x1 << 16);
+            if (MODE == PASS_REPAIR) {
+                const uint2 r = tr.cp[slot];
+                if (r.x == sv) {
+                    tr.done = true;
+                    tr.jstar = slot;
+                    bits += r.y;  // the rest of the trajectory is the recorded one
+                } else {
+                    tr.cp[slot] = make_uint2(sv, bits);
+                }
+            } else {
+                tr.cp[slot] = make_uint2(sv, bits);
+            }
+            slot -= 1u;
+            rem = tr.ckc - 1u;
+        } else {
+            rem -= 1u;
+        }
+    };
     if (pb & 7u) {  // partial topmost chunk
         const uint4 q = load_chunk(blk, n, (uint32_t)c_hi);
         enc_chunk<MODE, false>(q, (uint32_t)c_hi * 8u, pb, x0, x1, T, bits, em);
         if (MODE == PASS_EMIT && ck.base && (((uint32_t)c_hi * 8u) & ck.mask) == 0u)
             ckpt_record(ck, (uint32_t)c_hi * 8u, em.pos(), x0, x1);
+        if (TRACK) track();
         c_hi -= 1;
     }
-    if (c_hi < c_lo) return EncState{x0, x1, bits};
+    if (c_hi < c_lo || (MODE == PASS_REPAIR && tr.done)) return EncState{x0, x1, bits};
     auto ld = [&](int32_t c) { return v[c < c_lo ? c_lo : c]; };
     uint4 q0 = ld(c_hi), q1 = ld(c_hi - 1), q2 = ld(c_hi - 2), q3 = ld(c_hi - 3);
     auto body = [&](const uint4& q, int32_t c) {
         enc_chunk<MODE, true>(q, (uint32_t)c * 8u, pb, x0, x1, T, bits, em);
         if (MODE == PASS_EMIT && ck.base && (((uint32_t)c * 8u) & ck.mask) == 0u)
             ckpt_record(ck, (uint32_t)c * 8u, em.pos(), x0, x1);
+        if (TRACK) track();
     };
+    auto stop = [&](int32_t cn) { return cn < c_lo || (MODE == PASS_REPAIR && tr.done); };
     for (int32_t c = c_hi;; c -= 4) {
         body(q0, c);
-        if (c - 1 < c_lo) break;
+        if (stop(c - 1)) break;
         q0 = ld(c - 4);
         body(q1, c - 1);
-        if (c - 2 < c_lo) break;
+        if (stop(c - 2)) break;
         q1 = ld(c - 5);
         body(q2, c - 2);
-        if (c - 3 < c_lo) break;
+        if (stop(c - 3)) break;
         q2 = ld(c - 6);
         body(q3, c - 3);
-        if (c - 4 < c_lo) break;
+        if (stop(c - 4)) break;
         q3 = ld(c - 7);
     }
     return EncState{x0, x1, bits};
@@ -243,6 +299,7 @@ struct EncSmem {
             uint8_t sym_at[SIZE];
             uint8_t occ_sym[SIZE];
         } sp;
+        uint2 cp[64 * 8];  // phase 2: count-pass trajectories (Track), 8 slots per lane
     } tmp;
     uint32_t counts[256];
     int32_t norm[256];
@@ -354,30 +411,24 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     em.start(nullptr, 0);
     Ckpt ck{nullptr, 0, 0, 0, L};
 
-    // exact start of the top lane: init states (+ odd-length extra step)
-    // spec pass: lanes 1..ktop (the top lane runs exactly)
-    if (act && k >= 1) {
-        EncState e0 = (k == ktop) ? top_start<PASS_SPEC>(blk, n, tab, em) : EncState{1u << L, 1u << L, 0u};
-        e0 = enc_range<PASS_SPEC>(blk, n, pa, pb, e0, tab, em, ck);
-        sm.specF[b][k] = e0.x0 | (e0.x1 << 16);
-    }
-    __syncthreads();
-
-    FSE_STAMP(P, 5);
-    // count pass from the neighbour's spec end state, then verify: a lane's
-    // start must equal its neighbour's exact end state.  Iterating to the
-    // unique fixed point (the top lane is exact) makes every lane exact.
-    uint32_t start = (act && k < ktop) ? sm.specF[b][k + 1] : 0u;
+    // count pass: the top lane from its exact start (init states + the
+    // odd-length extra step), every other lane from a guessed start state,
+    // recording its trajectory.  Then verify against the neighbour's end
+    // state and repair by convergence (Track) until the fixed point.
+    Track tr{&sm.tmp.cp[lane * 8u], max(1u, (S / 8u + 7u) / 8u), false, 0u};
+    const uint32_t nslot = pb > pa ? (((pb - 1u) >> 3) - (pa >> 3)) / tr.ckc + 1u : 0u;
+    uint32_t start = (1u << L) | ((1u << L) << 16);
     uint32_t bits = 0;
-    bool need = act;
+    if (act) {
+        EncState e0 = (k == ktop) ? top_start<PASS_COUNT>(blk, n, tab, em) : EncState{1u << L, 1u << L, 0u};
+        e0 = enc_range<PASS_COUNT>(blk, n, pa, pb, e0, tab, em, ck, tr);
+        bits = e0.bits;
+        sm.cntF[b][k] = e0.x0 | (e0.x1 << 16);
+        track_fixup(tr, nslot, -1, bits);
+    }
+    FSE_STAMP(P, 5);
+    uint32_t n_iter = 0, n_rerun = 0;  // diagnostics (stamps counters)
     for (;;) {
-        if (need) {
-            EncState e0 = (k == ktop) ? top_start<PASS_COUNT>(blk, n, tab, em)
-                                      : EncState{start & 0xFFFFu, start >> 16, 0u};
-            e0 = enc_range<PASS_COUNT>(blk, n, pa, pb, e0, tab, em, ck);
-            bits = e0.bits + (k == 0 ? 2u * L + 1u : 0u);  // finals + marker (lib.rs:178-181)
-            sm.cntF[b][k] = e0.x0 | (e0.x1 << 16);
-        }
         __syncthreads();
         bool bad = false;
         uint32_t nbF = 0;
@@ -387,11 +438,23 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
         }
         __syncthreads();
         if (__ballot(bad) == 0) break;
-        if (bad) start = nbF;
-        need = bad;
+        ++n_iter;
+        n_rerun += (uint32_t)__popcll(__ballot(bad));
+        if (bad) {
+            start = nbF;
+            tr.done = false;
+            const EncState e0 = enc_range<PASS_REPAIR>(blk, n, pa, pb, EncState{start & 0xFFFFu, start >> 16, 0u},
+                                                       tab, em, ck, tr);
+            bits = e0.bits;
+            if (!tr.done) sm.cntF[b][k] = e0.x0 | (e0.x1 << 16);  // did not converge: new end state
+            track_fixup(tr, nslot, tr.done ? (int32_t)tr.jstar : -1, bits);
+        }
     }
+    if (k == 0) bits += 2u * L + 1u;  // finals + marker (lib.rs:178-181)
 
     FSE_STAMP(P, 6);
+    if (P.stamps && lane == 0)
+        P.stamps[(uint64_t)blockIdx.x * kStamps + kStamps - 1] = (uint64_t)n_iter | ((uint64_t)n_rerun << 32);
     // offsets: lane k writes after every lane j > k (stack order)
     const uint32_t hl = sm.info_hl[b];
     const uint32_t hdr_bits = hl * 8u;
@@ -413,7 +476,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     }
     __syncthreads();
     if (act && fits) {
-        em.start(gw, off);
+        em.start(gw, off, (uint32_t)(P.slot_bytes >> 2));
         if (P.sidecar && P.ckpt_interval) {
             ck.base = P.sidecar + gb * P.ckpt_per_block;
             ck.mask = P.ckpt_interval - 1u;
@@ -430,7 +493,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
         } else {
             e0 = EncState{start & 0xFFFFu, start >> 16, 0u};
         }
-        e0 = enc_range<PASS_EMIT>(blk, n, pa, pb, e0, tab, em, ck);
+        e0 = enc_range<PASS_EMIT>(blk, n, pa, pb, e0, tab, em, ck, tr);
         const uint32_t y0 = e0.x0, y1 = e0.x1;
         if (k == 0) {  // Encoder::finish x2 + marker (lib.rs:178-181)
             const uint32_t m = (1u << L) - 1u;
@@ -489,7 +552,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
                 if (wq != w) break;
                 v |= sm.mval[b][q];
             }
-            gw[w] = v;
+            if (w < (uint32_t)(P.slot_bytes >> 2)) gw[w] = v;
         }
     }
     FSE_STAMP(P, 8);
