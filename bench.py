@@ -39,6 +39,7 @@ def parse():
     ap.add_argument("--ckpt", type=int, default=128)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-c3", action="store_true", help="skip the decode-only (prebuilt tables) line")
     ap.add_argument("--gather", action="store_true",
                     help="after the timed steps, pack each rank's blocks on the GPU and gather the "
                          "compressed streams to rank 0 (RCCL); reported separately, never in value")
@@ -176,6 +177,27 @@ def main():
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         ok = bool(flag.item())
 
+    # C3 (BASELINE configs[2]): decode only, decode tables prebuilt and untimed
+    c3 = None
+    comp_bytes_pre = int(cb["comp_len"].to(torch.int64).sum())
+    if not args.no_c3:
+        tabs = codec.build_dtables(cb)
+        torch.cuda.synchronize(dev)
+        e3 = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        codec.decompress_dt_into(cb, tabs, out, dstat)
+        e3[0].record(stream)
+        for _ in range(args.steps):
+            codec.decompress_dt_into(cb, tabs, out, dstat)
+        e3[1].record(stream)
+        torch.cuda.synchronize(dev)
+        c3_ms = e3[0].elapsed_time(e3[1]) / args.steps
+        c3_ok = int(dstat.abs().max()) == 0 and bool(torch.equal(out, src))
+        c3 = {"workload": "C3-style decode only on the C2 blocks above (prebuilt decode tables, untimed): "
+                          f"{comp_bytes_pre / 2**30:.3f} GiB compressed -> {n / 2**30:.3f} GiB",
+              "decode_ms": round(c3_ms, 4), "decode_GiB_s": round(n / (c3_ms * 1e-3) / 2**30, 2),
+              "roofline_frac": None, "verified": c3_ok}
+        ok = ok and c3_ok
+
     gather_info = None
     if args.gather:
         from entropy_coders_amd.dist import gather_stream, pack_device
@@ -248,6 +270,9 @@ def main():
             "compressed_ratio": round(comp_bytes / n, 5),
             "verified_roundtrip": ok,
         }
+        if c3 is not None:
+            c3["roofline_frac"] = round(dec_bytes / (c3["decode_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+            line["c3_decode_only"] = c3
         if gather_info is not None:
             line["gather"] = gather_info
         if world == 1 and not args.no_cpu:

@@ -22,6 +22,47 @@ constexpr uint32_t kDefaultBlock = 65536;
 
 uint64_t round_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
+// Per-(device, stream, purpose) grow-only device scratch for the two-kernel
+// encode and decode: calls on one stream are ordered, so they may share it;
+// calls on different streams get different buffers.
+struct Scratch {
+    int dev;
+    void* stream;
+    int tag;
+    void* ptr;
+    uint64_t bytes;
+};
+std::mutex g_ws_mu;
+std::vector<Scratch> g_ws;
+
+void* scratch(void* stream, int tag, uint64_t bytes) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    Scratch* w = nullptr;
+    for (auto& x : g_ws)
+        if (x.dev == dev && x.stream == stream && x.tag == tag) w = &x;
+    if (!w) {
+        g_ws.push_back(Scratch{dev, stream, tag, nullptr, 0});
+        w = &g_ws.back();
+    }
+    if (w->bytes < bytes) {
+        if (w->ptr) {
+            (void)hipStreamSynchronize(static_cast<hipStream_t>(stream));
+            (void)hipFree(w->ptr);
+            w->ptr = nullptr;
+        }
+        if (hipMalloc(&w->ptr, bytes) != hipSuccess) {
+            w->bytes = 0;
+            w->ptr = nullptr;
+            return nullptr;
+        }
+        w->bytes = bytes;
+    }
+    return w->ptr;
+}
+enum { SCRATCH_DT = 1, SCRATCH_DTINFO = 2 };
+
 // Tuning / ablation knobs (not part of the ABI): FSEHIP_ENC_LANES=32|64,
 // FSEHIP_DEBUG bit mask (see fse_kernels.h).
 uint32_t env_u32(const char* name, uint32_t dflt) {
@@ -294,49 +335,6 @@ int fsehip_decompress_blocks_dt(const fsehip_params* p, const uint8_t* d_in, uin
                            0, stream, d_dtables, d_dtinfo);
 }
 
-// Per-(device, stream) decode-table workspace of the two-kernel decode
-// behind fsehip_decompress_blocks: calls on one stream are ordered, calls on
-// different streams get different buffers.  Grow-only.
-namespace {
-struct DtWorkspace {
-    uint32_t* dt = nullptr;
-    int32_t* info = nullptr;
-    uint64_t blocks = 0;
-    uint32_t lmax = 0;
-};
-std::mutex g_ws_mu;
-std::vector<std::pair<std::pair<int, void*>, DtWorkspace>> g_ws;
-
-DtWorkspace* workspace(void* stream, uint64_t n_blocks, uint32_t lmax) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    std::lock_guard<std::mutex> lk(g_ws_mu);
-    DtWorkspace* w = nullptr;
-    for (auto& kv : g_ws)
-        if (kv.first.first == dev && kv.first.second == stream) w = &kv.second;
-    if (!w) {
-        g_ws.push_back({{dev, stream}, DtWorkspace{}});
-        w = &g_ws.back().second;
-    }
-    if (w->blocks < n_blocks || w->lmax < lmax) {
-        if (w->dt) {
-            (void)hipStreamSynchronize(static_cast<hipStream_t>(stream));
-            (void)hipFree(w->dt);
-            (void)hipFree(w->info);
-            w->dt = nullptr;
-            w->info = nullptr;
-        }
-        w->blocks = std::max(w->blocks, n_blocks);
-        w->lmax = std::max(w->lmax, lmax);
-        if (hipMalloc(&w->dt, (4ull << w->lmax) * w->blocks) != hipSuccess ||
-            hipMalloc(&w->info, 4ull * w->blocks) != hipSuccess) {
-            w->blocks = 0;
-            return nullptr;
-        }
-    }
-    return w;
-}
-}  // namespace
 
 int fsehip_decompress_blocks(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
                              const uint32_t* d_comp_len, const uint64_t* d_sidecar, uint8_t* d_out, uint64_t n_total,
@@ -349,12 +347,13 @@ int fsehip_decompress_blocks(const fsehip_params* p, const uint8_t* d_in, uint64
         const uint32_t bs = p->block_size ? p->block_size : kDefaultBlock;
         const uint64_t n_blocks = (n_total + bs - 1) / bs;
         if (!device_ok()) return FSE_ERR_NO_DEVICE;
-        DtWorkspace* w = workspace(stream, n_blocks, dt_lmax(p));
-        if (!w) return FSE_ERR_HIP;
-        int rc = fsehip_build_dtables(p, d_in, slot_bytes, d_comp_len, (uint32_t)n_blocks, w->dt, w->info, stream);
+        uint32_t* dt = static_cast<uint32_t*>(scratch(stream, SCRATCH_DT, fsehip_dtable_bytes(p->max_table_log) * n_blocks));
+        int32_t* info = static_cast<int32_t*>(scratch(stream, SCRATCH_DTINFO, 4ull * n_blocks));
+        if (!dt || !info) return FSE_ERR_HIP;
+        int rc = fsehip_build_dtables(p, d_in, slot_bytes, d_comp_len, (uint32_t)n_blocks, dt, info, stream);
         if (rc != FSE_OK) return rc;
-        return fsehip_decompress_blocks_dt(p, d_in, slot_bytes, d_comp_len, d_sidecar, w->dt, w->info, d_out,
-                                           n_total, d_status, stream);
+        return fsehip_decompress_blocks_dt(p, d_in, slot_bytes, d_comp_len, d_sidecar, dt, info, d_out, n_total,
+                                           d_status, stream);
     }
     return decompress_impl(p, d_in, slot_bytes, d_comp_len, d_sidecar, d_out, n_total, nullptr, d_status, nullptr,
                            0, stream);
