@@ -202,16 +202,20 @@ def main():
     if args.gather:
         from entropy_coders_amd.dist import gather_stream, pack_device
 
+        packed, _ = pack_device(cb["out"], codec.slot_bytes, cb["comp_len"])  # warm-up (allocation)
+        del packed
         torch.cuda.synchronize(dev)
         barrier()
         g0 = time.perf_counter()
         packed, _ = pack_device(cb["out"], codec.slot_bytes, cb["comp_len"])
+        torch.cuda.synchronize(dev)
         tp = time.perf_counter()
         if world > 1:
             streams, _ = gather_stream(packed, cb["comp_len"], dst=0)
         torch.cuda.synchronize(dev)
         g1 = time.perf_counter()
         gather_info = {"packed_bytes_per_rank": int(packed.numel()),
+                       "pack_ms": round((tp - g0) * 1e3, 3),
                        "pack_plus_gather_ms": round((g1 - g0) * 1e3, 3),
                        "gather_GB_s": round(world * packed.numel() / max(g1 - tp, 1e-9) / 1e9, 2)
                        if world > 1 else None}

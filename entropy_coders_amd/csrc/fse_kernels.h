@@ -21,7 +21,7 @@ struct EncParams {
     uint64_t* sidecar;
     int32_t* status;
     uint32_t lanes;  // encoder lanes per block (32 or 64; 0 = default)
-    uint32_t debug;  // ablation: bit0 = tables only, bit1 = no emit pass
+    uint32_t debug;  // ablation: bit0 = tables only, bit1 = no emit pass, bit2 = no payload stores
     uint64_t* stamps;  // diagnostics: per-workgroup s_memtime at phase ends
 };
 

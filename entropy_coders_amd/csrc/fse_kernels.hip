@@ -420,7 +420,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     uint32_t start = (1u << L) | ((1u << L) << 16);
     uint32_t bits = 0;
     if (act) {
-        EncState e0 = (k == ktop) ? top_start<PASS_COUNT>(blk, n, tab, em) : EncState{1u << L, 1u << L, 0u};
+        EncState e0 = (k == ktop) ? top_start<PASS_COUNT>(blk, n, tab, em) : EncState{start & 0xFFFFu, start >> 16, 0u};
         e0 = enc_range<PASS_COUNT>(blk, n, pa, pb, e0, tab, em, ck, tr);
         bits = e0.bits;
         sm.cntF[b][k] = e0.x0 | (e0.x1 << 16);
@@ -476,7 +476,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     }
     __syncthreads();
     if (act && fits) {
-        em.start(gw, off, (uint32_t)(P.slot_bytes >> 2));
+        em.start(gw, off, (P.debug & 4u) ? 0u : (uint32_t)(P.slot_bytes >> 2));  // debug bit 2: no payload stores (ablation)
         if (P.sidecar && P.ckpt_interval) {
             ck.base = P.sidecar + gb * P.ckpt_per_block;
             ck.mask = P.ckpt_interval - 1u;
@@ -1299,16 +1299,29 @@ __global__ __launch_bounds__(256) void pack_blocks_kernel(const uint8_t* __restr
     if (b >= n_blocks) return;
     const uint32_t len = comp_len[b];
     uint8_t* slot = const_cast<uint8_t*>(slots) + b * slot_bytes;
-    uint8_t* s = stream + offsets[b];
+    const uint64_t o = offsets[b];
     if (!unpack) {
-        for (uint32_t i = threadIdx.x * 16u; i < len; i += 256u * 16u) {
-            const uint4 v = *reinterpret_cast<const uint4*>(slot + i);
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (uint32_t k = 0; k < 16u; ++k)
-                if (i + k < len) s[i + k] = (uint8_t)(w[k >> 2] >> (8u * (k & 3u)));
+        // dword-aligned stream writes; each from two aligned slot dwords
+        // (v_alignbyte); the partial dwords at both ends (shared with the
+        // neighbouring blocks) are written bytewise
+        const uint64_t d0 = (o + 3u) >> 2, d1 = (o + len) >> 2;  // full stream dwords [d0, d1)
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(slot);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(stream);
+        if (d1 > d0) {
+            const uint32_t head = (uint32_t)(4u * d0 - o);  // slot byte feeding stream dword d0
+            for (uint64_t d = d0 + threadIdx.x; d < d1; d += 256u) {
+                const uint32_t sb = head + 4u * (uint32_t)(d - d0);  // slot byte offset
+                const uint32_t q = sb >> 2, sh = sb & 3u;
+                const uint32_t lo = src[q], hi = src[q + 1u];  // slot slack covers q + 1
+                dst[d] = __builtin_amdgcn_alignbyte(hi, lo, sh);
+            }
         }
+        const uint64_t hb = min((uint64_t)len, 4u * d0 - o);  // head bytes before dword d0
+        if (threadIdx.x < hb) stream[o + threadIdx.x] = slot[threadIdx.x];
+        const uint64_t tb0 = d1 > d0 ? 4u * d1 - o : hb;  // tail bytes from here
+        for (uint64_t i = tb0 + threadIdx.x; i < len; i += 256u) stream[o + i] = slot[i];
     } else {
+        const uint8_t* s = stream + o;
         for (uint32_t i = threadIdx.x; i < len; i += 256u) slot[i] = s[i];
     }
 }
