@@ -291,6 +291,7 @@ static int decompress_impl(const fsehip_params* p, const uint8_t* d_in, uint64_t
     P.debug = env_u32("FSEHIP_DEBUG", 0) >> 4;
     P.waves = env_u32("FSEHIP_DEC_WAVES", 4) == 8 ? 8 : 4;
     P.variant = env_u32("FSEHIP_DEC_VAR", 2);
+    P.dual = env_u32("FSEHIP_DEC_DUAL", 0);
     // the decoder reads L from each header; size its tables for the bound
     uint32_t lmax = p->max_table_log ? p->max_table_log : 12;
     P.dt = d_dt;

@@ -45,7 +45,8 @@ struct DecParams {
     uint32_t waves;         // waves per block workgroup: 4 (default) or 8
     const uint32_t* dt;     // prebuilt decode tables [n_blocks][1 << lmax], or nullptr
     const int32_t* dtinfo;  // per block: header bytes | L << 16, or < 0 = status
-    uint32_t variant;       // LDS layout / reader: 3 = padded image (prebuilt tables), else linear window
+    uint32_t variant;       // LDS layout / reader: 3/5 = padded image (prebuilt tables), else linear window
+    uint32_t dual;          // two segments per lane, interleaved (prebuilt-table kernel)
 };
 
 // Decode-table build (header parse + DecodeTable) for a batch of blocks.

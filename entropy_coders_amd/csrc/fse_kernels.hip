@@ -709,7 +709,7 @@ __device__ __forceinline__ uint32_t lds_bits32_pad(const uint32_t* pay, int32_t 
 }
 template <int VAR>
 __device__ __forceinline__ uint32_t lds_bits(const uint32_t* pay, int32_t pos) {
-    return VAR == 3 ? lds_bits32_pad(pay, pos) : lds_bits32(pay, pos);
+    return (VAR == 3 || VAR == 5) ? lds_bits32_pad(pay, pos) : lds_bits32(pay, pos);
 }
 
 // Segment decode for a block staged in LDS.  One LdsChain = one segment's
@@ -756,6 +756,17 @@ struct LdsChain {
                 wlo = wnx;
                 wnx = pay[max((B >> 5) - 1, 0)];
             }
+        } else if (VAR == 5) {
+            // padded image + the window for this pair fetched together with
+            // the table entries (its <= 24 bits lie in [pos - 24, pos))
+            const int32_t lo = max(pos - 24, 0);
+            const uint32_t* wp = pay + pad_word((uint32_t)lo >> 5);
+            const uint32_t w0 = wp[0], w1 = wp[1];
+            const uint32_t base = (uint32_t)lo & ~31u;
+            e0 = *reinterpret_cast<const uint32_t*>(dtb + a0);
+            e1 = *reinterpret_cast<const uint32_t*>(dtb + a1);
+            pos -= (int32_t)((e0 + e1) & 0xFFu);
+            x = (uint32_t)((((uint64_t)w1 << 32) | w0) >> ((uint32_t)pos - base));
         } else if (VAR == 1) {
             const int32_t lo = max(pos - 24, 0);
             const uint32_t* wp = pay + ((uint32_t)lo >> 5);
@@ -845,6 +856,33 @@ __device__ __forceinline__ int32_t run_chain(LdsChain<VAR>& c, const uint32_t* p
         out[o++] = (uint8_t)dte_sym(e1);
     }
     return o == n ? FSE_OK : FSE_ERR_LENGTH_MISMATCH;
+}
+
+// Two segments per lane, interleaved pair by pair (independent state
+// chains: one chain's LDS and VALU latency hides behind the other's work).
+template <int VAR>
+__device__ __forceinline__ int32_t decode_dual(const uint32_t* pay, const uint8_t* dtb, LdsChain<VAR>& A, uint32_t pa,
+                                               uint32_t pa1, bool lastA, LdsChain<VAR>& Bc, uint32_t pb, uint32_t pb1,
+                                               bool lastB, uint32_t n, uint32_t Pm, uint8_t* __restrict__ out,
+                                               int32_t hdr_bits) {
+    const uint32_t common = min(pa1 - pa, pb1 - pb) / DEC_GROUP * DEC_GROUP;
+    for (uint32_t k = 0; k < common; k += DEC_GROUP) {
+        uint32_t wa[DEC_GROUP / 2u], wb[DEC_GROUP / 2u];
+#pragma unroll
+        for (uint32_t j = 0; j < DEC_GROUP; j += 2u) {
+            const uint32_t la = A.pair(pay, dtb);
+            const uint32_t lb = Bc.pair(pay, dtb);
+            const uint32_t ha = A.pair(pay, dtb);
+            const uint32_t hb = Bc.pair(pay, dtb);
+            wa[j >> 1] = __builtin_amdgcn_perm(ha, la, 0x05040100u);
+            wb[j >> 1] = __builtin_amdgcn_perm(hb, lb, 0x05040100u);
+        }
+        store_group(out + 2u * (pa + k), wa);
+        store_group(out + 2u * (pb + k), wb);
+    }
+    const int32_t ra = run_chain(A, pay, dtb, pa + common, pa1, lastA, n, Pm, out, hdr_bits);
+    const int32_t rb = run_chain(Bc, pay, dtb, pb + common, pb1, lastB, n, Pm, out, hdr_bits);
+    return ra != FSE_OK ? ra : rb;
 }
 
 // One workgroup of NW waves per block.  The compressed block (<= PMAX bytes)
@@ -1142,7 +1180,8 @@ __global__ __launch_bounds__(64 * NW) void decode_pre_kernel(DecParams P) {
     uint8_t* out = P.out + ooff;
     const int32_t info = P.dtinfo[gb];
     const uint32_t nwords = (clen + 3u) >> 2;
-    const bool in_lds = VAR == 3 ? (pad_word(nwords) + 2u) * 4u <= PMAX : clen <= PMAX;
+    constexpr bool PADDED = VAR == 3 || VAR == 5;
+    const bool in_lds = PADDED ? (pad_word(nwords) + 2u) * 4u <= PMAX : clen <= PMAX;
     FSE_STAMP(P, 0);
     if (info < 0 || n < 2) {
         if (tid == 0) P.status[gb] = info < 0 ? info : FSE_ERR_LENGTH_MISMATCH;
@@ -1152,7 +1191,7 @@ __global__ __launch_bounds__(64 * NW) void decode_pre_kernel(DecParams P) {
     const uint32_t L = (uint32_t)info >> 16;
     {  // stage the block image and the table
         if (in_lds) {
-            if (VAR == 3) {
+            if (PADDED) {
                 // dword LDS-DMA: LDS word d <- source word d - d/33
                 const uint32_t nd = pad_word(nwords) + 2u;
                 const uint32_t wmax = (uint32_t)min((uint64_t)nwords + 1u, P.slot_bytes / 4u) - 1u;
@@ -1191,6 +1230,31 @@ __global__ __launch_bounds__(64 * NW) void decode_pre_kernel(DecParams P) {
     const uint32_t maxbp = clen * 8u - (uint32_t)hdr_bits;
     const uint8_t* dtb = reinterpret_cast<const uint8_t*>(sm.dt);
     int32_t err = FSE_OK;
+    if (P.dual && in_lds) {  // two segments per lane: seg and seg + NT
+        for (uint32_t sa = tid; sa < nseg; sa += 2u * NT) {
+            const uint32_t sb = sa + NT;
+            const uint64_t ea = sc[sa];
+            const uint64_t eb = sb < nseg ? sc[sb] : ea;
+            if ((uint32_t)ea > maxbp || (uint32_t)eb > maxbp) {
+                err = FSE_ERR_BAD_ARG;
+                continue;
+            }
+            LdsChain<VAR> A, Bc;
+            A.init(sm.pay, hdr_bits + (int32_t)(uint32_t)ea, (uint32_t)(ea >> 32) & smask, (uint32_t)(ea >> 48) & smask);
+            const uint32_t pa = sa * I, pa1 = min(pa + I, Pm);
+            int32_t r;
+            if (sb < nseg) {
+                Bc.init(sm.pay, hdr_bits + (int32_t)(uint32_t)eb, (uint32_t)(eb >> 32) & smask,
+                        (uint32_t)(eb >> 48) & smask);
+                const uint32_t pb = sb * I, pb1 = min(pb + I, Pm);
+                r = decode_dual(sm.pay, dtb, A, pa, pa1, sa == nseg - 1u, Bc, pb, pb1, sb == nseg - 1u, n, Pm, out,
+                                hdr_bits);
+            } else {
+                r = run_chain(A, sm.pay, dtb, pa, pa1, sa == nseg - 1u, n, Pm, out, hdr_bits);
+            }
+            if (r != FSE_OK) err = r;
+        }
+    } else
     for (uint32_t seg = tid; seg < nseg; seg += NT) {
         const uint64_t e = sc[seg];
         const uint32_t p0 = seg * I, p1 = min(p0 + I, Pm);
@@ -1393,22 +1457,26 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
     const dim3 g(P.n_blocks);
     if (P.dt) {  // prebuilt tables: lean kernel; LDS = image + table (44 KB image -> 3 WG/CU)
         constexpr uint32_t PP = 44u << 10;
-        const bool pad = P.variant == 3;
+        auto go = [&](auto kern, uint32_t threads) { hipLaunchKernelGGL(kern, g, dim3(threads), 0, stream, P); };
         if (P.waves == 8) {
             if (lmax <= 11) {
-                if (pad) hipLaunchKernelGGL((decode_pre_kernel<11, 8, PP, 3>), g, dim3(512), 0, stream, P);
-                else hipLaunchKernelGGL((decode_pre_kernel<11, 8, PP, 2>), g, dim3(512), 0, stream, P);
+                if (P.variant == 3) go(decode_pre_kernel<11, 8, PP, 3>, 512);
+                else if (P.variant == 5) go(decode_pre_kernel<11, 8, PP, 5>, 512);
+                else go(decode_pre_kernel<11, 8, PP, 2>, 512);
             } else {
-                if (pad) hipLaunchKernelGGL((decode_pre_kernel<12, 8, PP - 8192, 3>), g, dim3(512), 0, stream, P);
-                else hipLaunchKernelGGL((decode_pre_kernel<12, 8, PP - 8192, 2>), g, dim3(512), 0, stream, P);
+                if (P.variant == 3) go(decode_pre_kernel<12, 8, PP - 8192, 3>, 512);
+                else if (P.variant == 5) go(decode_pre_kernel<12, 8, PP - 8192, 5>, 512);
+                else go(decode_pre_kernel<12, 8, PP - 8192, 2>, 512);
             }
         } else {
             if (lmax <= 11) {
-                if (pad) hipLaunchKernelGGL((decode_pre_kernel<11, 4, PP, 3>), g, dim3(256), 0, stream, P);
-                else hipLaunchKernelGGL((decode_pre_kernel<11, 4, PP, 2>), g, dim3(256), 0, stream, P);
+                if (P.variant == 3) go(decode_pre_kernel<11, 4, PP, 3>, 256);
+                else if (P.variant == 5) go(decode_pre_kernel<11, 4, PP, 5>, 256);
+                else go(decode_pre_kernel<11, 4, PP, 2>, 256);
             } else {
-                if (pad) hipLaunchKernelGGL((decode_pre_kernel<12, 4, PP - 8192, 3>), g, dim3(256), 0, stream, P);
-                else hipLaunchKernelGGL((decode_pre_kernel<12, 4, PP - 8192, 2>), g, dim3(256), 0, stream, P);
+                if (P.variant == 3) go(decode_pre_kernel<12, 4, PP - 8192, 3>, 256);
+                else if (P.variant == 5) go(decode_pre_kernel<12, 4, PP - 8192, 5>, 256);
+                else go(decode_pre_kernel<12, 4, PP - 8192, 2>, 256);
             }
         }
         return hipGetLastError();
