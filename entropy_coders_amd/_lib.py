@@ -20,6 +20,7 @@ EXPORTS = (
     "fsehip_generate", "fsehip_device_count", "fsehip_version",
     "fsehip_pack_blocks", "fsehip_unpack_blocks",
     "fsehip_dtable_bytes", "fsehip_build_dtables", "fsehip_decompress_blocks_dt",
+    "fse_compress", "fse_decompress", "fsehip_sidecar_per_block_ns",
 )
 
 STATUS = {
@@ -41,7 +42,8 @@ class FseError(Exception):
 
 class Params(C.Structure):
     _fields_ = [("block_size", C.c_uint32), ("table_log", C.c_uint32),
-                ("ckpt_interval", C.c_uint32), ("max_table_log", C.c_uint32)]
+                ("ckpt_interval", C.c_uint32), ("max_table_log", C.c_uint32),
+                ("nstates", C.c_uint32)]
 
 
 _lib = None
@@ -59,11 +61,15 @@ def load() -> C.CDLL:
     lib.fse_compress2.argtypes = [P, sz, P, sz, C.POINTER(sz), C.POINTER(u64)]
     lib.fse_compress2_log.argtypes = [P, sz, u32, P, sz, C.POINTER(sz), C.POINTER(u64)]
     lib.fse_decompress2.argtypes = [P, sz, P, sz, C.POINTER(sz)]
+    lib.fse_compress.argtypes = [P, sz, P, sz, C.POINTER(sz), C.POINTER(u64)]
+    lib.fse_decompress.argtypes = [P, sz, P, sz, C.POINTER(sz)]
     lib.histogram_count.argtypes = [P, sz, P, C.POINTER(u32)]
     lib.fsehip_slot_bytes.argtypes = [u32, u32]
     lib.fsehip_slot_bytes.restype = u64
     lib.fsehip_sidecar_per_block.argtypes = [u32, u32]
     lib.fsehip_sidecar_per_block.restype = u32
+    lib.fsehip_sidecar_per_block_ns.argtypes = [u32, u32, u32]
+    lib.fsehip_sidecar_per_block_ns.restype = u32
     lib.fsehip_compress_blocks.argtypes = [C.POINTER(Params), P, u64, P, u64, P, P, P, P, P]
     lib.fsehip_decompress_blocks.argtypes = [C.POINTER(Params), P, u64, P, P, P, u64, P, P]
     lib.fsehip_build_sidecar.argtypes = [C.POINTER(Params), P, u64, P, P, u64, P, P, P]

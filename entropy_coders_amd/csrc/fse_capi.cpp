@@ -169,13 +169,14 @@ struct Meta {
 };
 
 int compress_one(const uint8_t* src, size_t n, uint32_t table_log, uint8_t* dst, size_t dst_cap, size_t* dst_len,
-                 uint64_t* payload_bits) {
+                 uint64_t* payload_bits, uint32_t nstates = 2) {
     if (!dst_len) return FSE_ERR_BAD_ARG;
     if (n == 0) return FSE_ERR_EMPTY;  // size.ilog2() panics (histogram.rs:266)
     if (n > (1u << 28)) return FSE_ERR_UNSUPPORTED;
     if (table_log > 12) return FSE_ERR_UNSUPPORTED;
     if (!device_ok()) return FSE_ERR_NO_DEVICE;
-    fsehip_params p{(uint32_t)round_up(n, 16), table_log, 0, table_log ? std::max<uint32_t>(table_log, 11) : 11};
+    fsehip_params p{(uint32_t)round_up(n, 16), table_log, 0, table_log ? std::max<uint32_t>(table_log, 11) : 11,
+                    nstates};
     const uint64_t slot = fsehip_slot_bytes(p.block_size, p.max_table_log);
     uint8_t* d_src = g_stage.get(0, round_up(n, 16) + 16);
     uint8_t* d_out = g_stage.get(1, slot);
@@ -213,6 +214,11 @@ uint32_t fsehip_sidecar_per_block(uint32_t block_size, uint32_t ckpt_interval) {
     return block_size / 2u / ckpt_interval + 2u;
 }
 
+uint32_t fsehip_sidecar_per_block_ns(uint32_t block_size, uint32_t ckpt_interval, uint32_t nstates) {
+    if (ckpt_interval == 0) return 0;
+    return nstates == 1 ? block_size / ckpt_interval + 2u : block_size / 2u / ckpt_interval + 2u;
+}
+
 int fsehip_device_count(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -234,23 +240,27 @@ int fsehip_compress_blocks(const fsehip_params* p, const uint8_t* d_src, uint64_
     const uint32_t lmax = lmax_for(p);
     if (lmax > 12) return FSE_ERR_UNSUPPORTED;
     if (slot_bytes & 15u) return FSE_ERR_BAD_ARG;
-    if (p->ckpt_interval && (p->ckpt_interval < 8 || (p->ckpt_interval & (p->ckpt_interval - 1)))) return FSE_ERR_BAD_ARG;
+    const uint32_t ns = p->nstates == 1 ? 1u : 2u;
+    if (p->nstates > 2) return FSE_ERR_BAD_ARG;
+    if (p->ckpt_interval && (p->ckpt_interval < (ns == 1 ? 16u : 8u) || (p->ckpt_interval & (p->ckpt_interval - 1))))
+        return FSE_ERR_BAD_ARG;
     if (!device_ok()) return FSE_ERR_NO_DEVICE;
     fsehip::EncParams P{};
+    P.nstates = ns;
     P.src = d_src;
     P.n_total = n_total;
     P.block_size = bs;
     P.n_blocks = (uint32_t)n_blocks;
     P.table_log = p->table_log;
     P.ckpt_interval = d_sidecar ? p->ckpt_interval : 0;
-    P.ckpt_per_block = fsehip_sidecar_per_block(bs, P.ckpt_interval);
+    P.ckpt_per_block = fsehip_sidecar_per_block_ns(bs, P.ckpt_interval, ns);
     P.out = d_out;
     P.slot_bytes = slot_bytes;
     P.comp_len = d_comp_len;
     P.payload_bits = d_payload_bits;
     P.sidecar = P.ckpt_interval ? d_sidecar : nullptr;
     P.status = d_status;
-    P.lanes = env_u32("FSEHIP_ENC_LANES", 64) == 32 ? 32 : 64;
+    P.lanes = (ns == 2 && env_u32("FSEHIP_ENC_LANES", 64) == 32) ? 32 : 64;
     P.debug = env_u32("FSEHIP_DEBUG", 0);
     const size_t groups = (n_blocks * P.lanes + 63) / 64;
     P.stamps = g_stamps_enc.get(groups);
@@ -269,17 +279,21 @@ static int decompress_impl(const fsehip_params* p, const uint8_t* d_in, uint64_t
     const uint64_t n_blocks = n_total ? (n_total + bs - 1) / bs : 1;
     if (n_blocks > 1 && (bs & 15u)) return FSE_ERR_BAD_ARG;
     if (slot_bytes & 3u) return FSE_ERR_BAD_ARG;
+    const uint32_t ns = p->nstates == 1 ? 1u : 2u;
+    if (p->nstates > 2) return FSE_ERR_BAD_ARG;
     if ((d_sidecar || d_sidecar_out) &&
-        (p->ckpt_interval < 8 || (p->ckpt_interval & (p->ckpt_interval - 1))))
+        (p->ckpt_interval < (ns == 1 ? 16u : 8u) || (p->ckpt_interval & (p->ckpt_interval - 1))))
         return FSE_ERR_BAD_ARG;
+    if (ns == 1 && (!d_dt || d_sidecar_out)) return FSE_ERR_UNSUPPORTED;  // 1-state runs on prebuilt tables only
     if (!device_ok()) return FSE_ERR_NO_DEVICE;
     fsehip::DecParams P{};
+    P.nstates = ns;
     P.in = d_in;
     P.slot_bytes = slot_bytes;
     P.comp_len = d_comp_len;
     P.sidecar = d_sidecar;
     P.ckpt_interval = p->ckpt_interval;
-    P.ckpt_per_block = fsehip_sidecar_per_block(bs, p->ckpt_interval);
+    P.ckpt_per_block = fsehip_sidecar_per_block_ns(bs, p->ckpt_interval, ns);
     P.out = d_out;
     P.n_total = n_total;
     P.block_size = bs;
@@ -329,7 +343,8 @@ int fsehip_decompress_blocks_dt(const fsehip_params* p, const uint8_t* d_in, uin
                                 const int32_t* d_dtinfo, uint8_t* d_out, uint64_t n_total, int32_t* d_status,
                                 fsehip_stream_t stream) {
     if (n_total == 0) return FSE_ERR_EMPTY;
-    if (!p || !d_sidecar || !d_dtables || !d_dtinfo || p->ckpt_interval == 0) return FSE_ERR_BAD_ARG;
+    if (!p || !d_dtables || !d_dtinfo) return FSE_ERR_BAD_ARG;
+    if ((!d_sidecar || p->ckpt_interval == 0) && p->nstates != 1) return FSE_ERR_BAD_ARG;  // 1-state: serial without one
     fsehip_params q = *p;
     q.max_table_log = dt_lmax(p);  // the table stride the tables were built with
     return decompress_impl(&q, d_in, slot_bytes, d_comp_len, d_sidecar, d_out, n_total, nullptr, d_status, nullptr,
@@ -342,7 +357,7 @@ int fsehip_decompress_blocks(const fsehip_params* p, const uint8_t* d_in, uint64
                              int32_t* d_status, fsehip_stream_t stream) {
     if (n_total == 0) return FSE_ERR_EMPTY;
     if (d_sidecar && p && p->ckpt_interval == 0) return FSE_ERR_BAD_ARG;
-    if (d_sidecar && p && !env_u32("FSEHIP_DEC_FUSED", 0)) {
+    if (p && (p->nstates == 1 || (d_sidecar && !env_u32("FSEHIP_DEC_FUSED", 0)))) {
         // two kernels: decode tables for all blocks at high occupancy, then
         // the LDS-heavy segment decode with no serial phase
         const uint32_t bs = p->block_size ? p->block_size : kDefaultBlock;
@@ -463,6 +478,45 @@ int fse_decompress2(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, 
     fsehip_params p{0, 0, 0, 12};
     int rc = decompress_impl(&p, d_in, padded, &m->comp_len, nullptr, d_out, 0, nullptr, &m->status,
                              &m->payload_bits, (uint32_t)cap64, nullptr);
+    if (rc) return rc;
+    Meta h{};
+    if (hipMemcpy(&h, d_meta, sizeof(Meta), hipMemcpyDeviceToHost) != hipSuccess) return FSE_ERR_HIP;
+    if (h.status != FSE_OK) return h.status;
+    const uint32_t out_len = h.payload_bits;  // decoded byte count
+    if (out_len && hipMemcpy(dst + *dst_len, d_out, out_len, hipMemcpyDeviceToHost) != hipSuccess) return FSE_ERR_HIP;
+    *dst_len += out_len;
+    return FSE_OK;
+}
+
+int fse_compress(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, size_t* dst_len, uint64_t* payload_bits) {
+    // lib.rs:112-143; n == 1 is valid here (a lone seed state), unlike fse_compress2
+    return compress_one(src, n, 0, dst, dst_cap, dst_len, payload_bits, 1);
+}
+
+int fse_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, size_t* dst_len) {
+    if (!dst_len || *dst_len > dst_cap) return FSE_ERR_BAD_ARG;
+    if (n == 0) return FSE_ERR_EMPTY;  // BitStreamReader::new asserts (stream_reader.rs:17)
+    if (n > (1u << 30)) return FSE_ERR_UNSUPPORTED;
+    if (!device_ok()) return FSE_ERR_NO_DEVICE;
+    const uint64_t padded = round_up(n + 16, 256);
+    const uint64_t cap64 = std::min<uint64_t>(dst_cap - *dst_len, 0x7FFFFFFFu);
+    uint8_t* d_in = g_stage.get(0, padded);
+    uint8_t* d_out = g_stage.get(1, std::max<uint64_t>(cap64, 16));
+    uint8_t* d_meta = g_stage.get(2, sizeof(Meta));
+    uint8_t* d_dt = g_stage.get(3, fsehip_dtable_bytes(12) + 16);
+    if (!d_in || !d_out || !d_meta || !d_dt) return FSE_ERR_HIP;
+    if (hipMemset(d_in, 0, padded) != hipSuccess) return FSE_ERR_HIP;
+    if (hipMemcpy(d_in, src, n, hipMemcpyHostToDevice) != hipSuccess) return FSE_ERR_HIP;
+    Meta* m = reinterpret_cast<Meta*>(d_meta);
+    Meta h0{(uint32_t)n, 0, 0, 0};
+    if (hipMemcpy(d_meta, &h0, sizeof(Meta), hipMemcpyHostToDevice) != hipSuccess) return FSE_ERR_HIP;
+    fsehip_params p{0, 0, 0, 12, 1};
+    uint32_t* dt = reinterpret_cast<uint32_t*>(d_dt);
+    int32_t* info = reinterpret_cast<int32_t*>(d_dt + fsehip_dtable_bytes(12));
+    int rc = fsehip_build_dtables(&p, d_in, padded, &m->comp_len, 1, dt, info, nullptr);
+    if (rc) return rc;
+    rc = decompress_impl(&p, d_in, padded, &m->comp_len, nullptr, d_out, 0, nullptr, &m->status, &m->payload_bits,
+                         (uint32_t)cap64, nullptr, dt, info);
     if (rc) return rc;
     Meta h{};
     if (hipMemcpy(&h, d_meta, sizeof(Meta), hipMemcpyDeviceToHost) != hipSuccess) return FSE_ERR_HIP;

@@ -21,6 +21,7 @@ struct EncParams {
     uint64_t* sidecar;
     int32_t* status;
     uint32_t lanes;  // encoder lanes per block (32 or 64; 0 = default)
+    uint32_t nstates;  // 2 = fse_compress2 (default), 1 = fse_compress
     uint32_t debug;  // ablation: bit0 = tables only, bit1 = no emit pass, bit2 = no payload stores
     uint64_t* stamps;  // diagnostics: per-workgroup s_memtime at phase ends
 };
@@ -47,6 +48,7 @@ struct DecParams {
     const int32_t* dtinfo;  // per block: header bytes | L << 16, or < 0 = status
     uint32_t variant;       // LDS layout / reader: 3/5 = padded image (prebuilt tables), else linear window
     uint32_t dual;          // two segments per lane, interleaved (prebuilt-table kernel)
+    uint32_t nstates;       // 2 = fse_compress2 blocks (default), 1 = fse_compress blocks
 };
 
 // Decode-table build (header parse + DecodeTable) for a batch of blocks.

@@ -136,10 +136,11 @@ __device__ __forceinline__ uint32_t enc_step(uint32_t& x, uint32_t s, const EncT
     return nb;
 }
 
-// One 16-byte chunk = pairs c8+7 .. c8 (lib.rs:167-176: E1 then E0 per
-// pair).  FULL chunks need no guard; only the topmost chunk of the topmost
-// lane can extend past the last main-loop pair pb.
-template <int MODE, bool FULL>
+// One 16-byte chunk.  NS = 2 (fse_compress2): pairs c8+7 .. c8 (lib.rs:167-176:
+// E1 then E0 per pair).  NS = 1 (fse_compress): symbols c8+15 .. c8 with one
+// state (lib.rs:127-138).  FULL chunks need no guard; only the topmost chunk
+// of the topmost lane can extend past the last main-loop step pb.
+template <int MODE, bool FULL, int NS>
 __device__ __forceinline__ void enc_chunk(const uint4& q, uint32_t c8, uint32_t pb, uint32_t& x0, uint32_t& x1,
                                           const EncTab& T, uint32_t& bits, Emit& em) {
     const uint32_t w[4] = {q.x, q.y, q.z, q.w};
@@ -151,6 +152,23 @@ __device__ __forceinline__ void enc_chunk(const uint4& q, uint32_t c8, uint32_t 
         const uint32_t sh = 16u * (uint32_t)(j & 1);
         t0[j] = T.tt[(w[j >> 1] >> sh) & 0xFFu];
         t1[j] = T.tt[(w[j >> 1] >> (sh + 8u)) & 0xFFu];
+    }
+    if (NS == 1) {
+#pragma unroll
+        for (int j = 15; j >= 0; --j) {
+            if (!FULL && c8 + (uint32_t)j >= pb) continue;
+            const uint2 t = (j & 1) ? t1[j >> 1] : t0[j >> 1];
+            const uint32_t v0 = x0;
+            const uint32_t nb0 = (t.x + x0) >> 16;
+            x0 = *reinterpret_cast<const uint16_t*>(T.st + ((x0 >> nb0) << 1) + (int32_t)t.y);
+            if (MODE == PASS_COUNT || MODE == PASS_REPAIR) bits += nb0;
+            if (MODE == PASS_EMIT) {
+                em.put(v0 & ((1u << nb0) - 1u), nb0);
+                if (j & 1) em.flush();  // <= 2 x 12 bits between flushes
+            }
+        }
+        if (MODE == PASS_EMIT) em.flush();
+        return;
     }
 #pragma unroll
     for (int j = 7; j >= 0; --j) {
@@ -171,9 +189,11 @@ __device__ __forceinline__ void enc_chunk(const uint4& q, uint32_t c8, uint32_t 
 
 // Sidecar entry for the decoder state before pair p (= encoder state after
 // encoding pair p): bit position (payload-relative) and both states.
+// (NS = 1: one state, s1 = 0.)
+template <int NS>
 __device__ __forceinline__ void ckpt_record(const Ckpt& ck, uint32_t p, uint32_t pos, uint32_t x0, uint32_t x1) {
     ck.base[p >> ck.shift] = (uint64_t)(pos - ck.hdr_bits) | ((uint64_t)(x0 - (1u << ck.L)) << 32) |
-                             ((uint64_t)(x1 - (1u << ck.L)) << 48);
+                             (NS == 2 ? ((uint64_t)(x1 - (1u << ck.L)) << 48) : 0ull);
 }
 
 // Encode pairs pb-1 down to pa.  Source chunks (16 B = 8 pairs) stream
@@ -181,15 +201,16 @@ __device__ __forceinline__ void ckpt_record(const Ckpt& ck, uint32_t p, uint32_t
 // so three loads stay in flight and no register copy forces an early
 // s_waitcnt.  Loads are unconditional (the index is clamped to the
 // segment); the partial topmost chunk is peeled and loaded byte-wise.
-template <int MODE>
+template <int MODE, int NS>
 __device__ __forceinline__ EncState enc_range(const uint8_t* __restrict__ blk, uint32_t n, uint32_t pa, uint32_t pb,
                                               EncState st, const EncTab& T, Emit& em, const Ckpt& ck, Track& tr) {
     constexpr bool TRACK = MODE == PASS_COUNT || MODE == PASS_REPAIR;
     uint32_t x0 = st.x0, x1 = st.x1, bits = st.bits;
     if (pb <= pa) return st;
     const uint4* v = reinterpret_cast<const uint4*>(blk);
-    int32_t c_hi = (int32_t)((pb - 1u) >> 3);
-    const int32_t c_lo = (int32_t)(pa >> 3);
+    constexpr uint32_t CS = NS == 2 ? 3u : 4u;  // log2 steps per 16-byte chunk
+    int32_t c_hi = (int32_t)((pb - 1u) >> CS);
+    const int32_t c_lo = (int32_t)(pa >> CS);
     // checkpoint after chunk c when (c - c_lo) % ckc == 0; slot (c - c_lo) / ckc
     uint32_t rem = 0, slot = 0;
     if (TRACK) {
@@ -217,11 +238,11 @@ __device__ __forceinline__ EncState enc_range(const uint8_t* __restrict__ blk, u
             rem -= 1u;
         }
     };
-    if (pb & 7u) {  // partial topmost chunk
+    if (pb & ((1u << CS) - 1u)) {  // partial topmost chunk
         const uint4 q = load_chunk(blk, n, (uint32_t)c_hi);
-        enc_chunk<MODE, false>(q, (uint32_t)c_hi * 8u, pb, x0, x1, T, bits, em);
-        if (MODE == PASS_EMIT && ck.base && (((uint32_t)c_hi * 8u) & ck.mask) == 0u)
-            ckpt_record(ck, (uint32_t)c_hi * 8u, em.pos(), x0, x1);
+        enc_chunk<MODE, false, NS>(q, (uint32_t)c_hi << CS, pb, x0, x1, T, bits, em);
+        if (MODE == PASS_EMIT && ck.base && (((uint32_t)c_hi << CS) & ck.mask) == 0u)
+            ckpt_record<NS>(ck, (uint32_t)c_hi << CS, em.pos(), x0, x1);
         if (TRACK) track();
         c_hi -= 1;
     }
@@ -229,9 +250,9 @@ __device__ __forceinline__ EncState enc_range(const uint8_t* __restrict__ blk, u
     auto ld = [&](int32_t c) { return v[c < c_lo ? c_lo : c]; };
     uint4 q0 = ld(c_hi), q1 = ld(c_hi - 1), q2 = ld(c_hi - 2), q3 = ld(c_hi - 3);
     auto body = [&](const uint4& q, int32_t c) {
-        enc_chunk<MODE, true>(q, (uint32_t)c * 8u, pb, x0, x1, T, bits, em);
-        if (MODE == PASS_EMIT && ck.base && (((uint32_t)c * 8u) & ck.mask) == 0u)
-            ckpt_record(ck, (uint32_t)c * 8u, em.pos(), x0, x1);
+        enc_chunk<MODE, true, NS>(q, (uint32_t)c << CS, pb, x0, x1, T, bits, em);
+        if (MODE == PASS_EMIT && ck.base && (((uint32_t)c << CS) & ck.mask) == 0u)
+            ckpt_record<NS>(ck, (uint32_t)c << CS, em.pos(), x0, x1);
         if (TRACK) track();
     };
     auto stop = [&](int32_t cn) { return cn < c_lo || (MODE == PASS_REPAIR && tr.done); };
@@ -260,12 +281,19 @@ __device__ __forceinline__ uint32_t enc_init(const EncTab& T, uint32_t s) {
     return *reinterpret_cast<const uint16_t*>(T.st + ((v >> bo) << 1) + (int32_t)t.y);
 }
 
-// Exact state of the topmost lane before the main loop: both encoders seeded
-// with the last symbols, plus the odd-length extra step (lib.rs:153-165).
-template <int MODE>
+// Exact state of the topmost lane before the main loop.  NS = 2: both
+// encoders seeded with the last symbols, plus the odd-length extra step
+// (lib.rs:153-165).  NS = 1: the state seeded with the last symbol; the
+// main loop then covers symbols n-2 .. 0 (lib.rs:120-126).
+template <int MODE, int NS>
 __device__ __forceinline__ EncState top_start(const uint8_t* blk, uint32_t n, const EncTab& tab, Emit& em) {
     EncState e;
     e.bits = 0;
+    if (NS == 1) {
+        e.x0 = enc_init(tab, blk[n - 1u]);
+        e.x1 = 0;  // unused; 0 in every lane so packed states compare equal
+        return e;
+    }
     if (n & 1u) {  // lib.rs:155-160
         e.x0 = enc_init(tab, blk[n - 1u]);
         e.x1 = enc_init(tab, blk[n - 2u]);
@@ -315,7 +343,7 @@ struct EncSmem {
     int scratch[4];
 };
 
-template <int LMAX, int T>
+template <int LMAX, int T, int NS>
 __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     constexpr int BPW = 64 / T;
     __shared__ EncSmem<LMAX, T> sm;
@@ -401,9 +429,11 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     const uint8_t* blk = P.src + boff;
     const uint32_t L = sm.info_L[b];
     const EncTab tab{reinterpret_cast<const uint8_t*>(sm.st[b]), sm.tt[b]};
-    const uint32_t Pm = live ? ((n & 1u) ? (n - 3u) / 2u : n / 2u - 1u) : 0u;
+    // main-loop steps: pairs (NS = 2) or symbols below the seed (NS = 1)
+    const uint32_t Pm = live ? (NS == 2 ? ((n & 1u) ? (n - 3u) / 2u : n / 2u - 1u) : n - 1u) : 0u;
+    constexpr uint32_t SPC = NS == 2 ? 8u : 16u;  // steps per 16-byte chunk
     uint32_t S = (Pm + T - 1u) / T;
-    S = max(8u, (S + 7u) & ~7u);
+    S = max(SPC, (S + SPC - 1u) & ~(SPC - 1u));
     const uint32_t ktop = Pm ? (Pm - 1u) / S : 0u;
     const bool act = live && k <= ktop;
     const uint32_t pa = k * S, pb = min(pa + S, Pm);
@@ -415,13 +445,13 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     // odd-length extra step), every other lane from a guessed start state,
     // recording its trajectory.  Then verify against the neighbour's end
     // state and repair by convergence (Track) until the fixed point.
-    Track tr{&sm.tmp.cp[lane * 8u], max(1u, (S / 8u + 7u) / 8u), false, 0u};
-    const uint32_t nslot = pb > pa ? (((pb - 1u) >> 3) - (pa >> 3)) / tr.ckc + 1u : 0u;
-    uint32_t start = (1u << L) | ((1u << L) << 16);
+    Track tr{&sm.tmp.cp[lane * 8u], max(1u, (S / SPC + 7u) / 8u), false, 0u};
+    const uint32_t nslot = pb > pa ? (((pb - 1u) / SPC) - (pa / SPC)) / tr.ckc + 1u : 0u;
+    uint32_t start = (1u << L) | (NS == 2 ? (1u << L) << 16 : 0u);
     uint32_t bits = 0;
     if (act) {
-        EncState e0 = (k == ktop) ? top_start<PASS_COUNT>(blk, n, tab, em) : EncState{start & 0xFFFFu, start >> 16, 0u};
-        e0 = enc_range<PASS_COUNT>(blk, n, pa, pb, e0, tab, em, ck, tr);
+        EncState e0 = (k == ktop) ? top_start<PASS_COUNT, NS>(blk, n, tab, em) : EncState{start & 0xFFFFu, start >> 16, 0u};
+        e0 = enc_range<PASS_COUNT, NS>(blk, n, pa, pb, e0, tab, em, ck, tr);
         bits = e0.bits;
         sm.cntF[b][k] = e0.x0 | (e0.x1 << 16);
         track_fixup(tr, nslot, -1, bits);
@@ -443,14 +473,14 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
         if (bad) {
             start = nbF;
             tr.done = false;
-            const EncState e0 = enc_range<PASS_REPAIR>(blk, n, pa, pb, EncState{start & 0xFFFFu, start >> 16, 0u},
+            const EncState e0 = enc_range<PASS_REPAIR, NS>(blk, n, pa, pb, EncState{start & 0xFFFFu, start >> 16, 0u},
                                                        tab, em, ck, tr);
             bits = e0.bits;
             if (!tr.done) sm.cntF[b][k] = e0.x0 | (e0.x1 << 16);  // did not converge: new end state
             track_fixup(tr, nslot, tr.done ? (int32_t)tr.jstar : -1, bits);
         }
     }
-    if (k == 0) bits += 2u * L + 1u;  // finals + marker (lib.rs:178-181)
+    if (k == 0) bits += (uint32_t)NS * L + 1u;  // finals + marker (lib.rs:178-181 / 139-141)
 
     FSE_STAMP(P, 6);
     if (P.stamps && lane == 0)
@@ -485,20 +515,20 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
         }
         EncState e0;
         if (k == ktop) {
-            e0 = top_start<PASS_EMIT>(blk, n, tab, em);
-            if (ck.base && (Pm & ck.mask) == 0u) {  // checkpoint "before pair Pm"
-                ck.base[Pm >> ck.shift] = (uint64_t)(em.pos() - hdr_bits) | ((uint64_t)(e0.x0 - (1u << L)) << 32) |
-                                          ((uint64_t)(e0.x1 - (1u << L)) << 48);
-            }
+            e0 = top_start<PASS_EMIT, NS>(blk, n, tab, em);
+            if (ck.base && (Pm & ck.mask) == 0u)  // checkpoint "before step Pm"
+                ckpt_record<NS>(ck, Pm, em.pos(), e0.x0, e0.x1);
         } else {
             e0 = EncState{start & 0xFFFFu, start >> 16, 0u};
         }
-        e0 = enc_range<PASS_EMIT>(blk, n, pa, pb, e0, tab, em, ck, tr);
+        e0 = enc_range<PASS_EMIT, NS>(blk, n, pa, pb, e0, tab, em, ck, tr);
         const uint32_t y0 = e0.x0, y1 = e0.x1;
-        if (k == 0) {  // Encoder::finish x2 + marker (lib.rs:178-181)
+        if (k == 0) {  // Encoder::finish (x2 for NS = 2) + marker (lib.rs:178-181 / 139-141)
             const uint32_t m = (1u << L) - 1u;
-            em.put(y1 & m, L);
-            em.flush();
+            if (NS == 2) {
+                em.put(y1 & m, L);
+                em.flush();
+            }
             em.put(y0 & m, L);
             em.flush();
             em.put(1u, 1u);
@@ -1159,6 +1189,80 @@ __global__ __launch_bounds__(64 * NW) void decode_blocks_kernel(DecParams P) {
 // and its LDS is the block image plus the table.  VAR 3 stages the block as
 // the padded image (pad_word), VAR 2 linearly with per-lane windows.
 // ------------------------------------------------------------------------
+// ------------------------------------------------------------------------
+// 1-state decode (fse_decompress, lib.rs:187-211): one state chain, one
+// symbol per step, same tables and sidecar layout (s1 = 0).  The per-lane
+// window reader is the VAR 2 one.
+// ------------------------------------------------------------------------
+struct LdsChain1 {
+    int32_t pos, B;
+    uint32_t wlo, whi, wnx, a;
+    __device__ __forceinline__ void init(const uint32_t* pay, int32_t p, uint32_t s) {
+        pos = p;
+        a = s << 2;
+        const int32_t k = max((p >> 5) - 1, 0);
+        B = k << 5;
+        wlo = pay[k];
+        whi = pay[k + 1];
+        wnx = pay[max(k - 1, 0)];
+    }
+    // one symbol; returns the table entry (symbol in bits 8-15)
+    __device__ __forceinline__ uint32_t step(const uint32_t* pay, const uint8_t* dtb) {
+        const uint32_t e = *reinterpret_cast<const uint32_t*>(dtb + a);
+        pos -= (int32_t)(e & 0xFFu);
+        const uint32_t x = (uint32_t)((((uint64_t)whi << 32) | wlo) >> (uint32_t)(pos - B));
+        if (pos < B + 32) {
+            B -= 32;
+            whi = wlo;
+            wlo = wnx;
+            wnx = pay[max((B >> 5) - 1, 0)];
+        }
+        a = (e >> 16) + (__builtin_amdgcn_ubfe(x, 0u, e) << 2);
+        return e;
+    }
+};
+
+// Steps [p, p1) of one 1-state segment; the last segment then emits the
+// final state's symbol if, as in the reference loop, the next read fails.
+__device__ __forceinline__ int32_t run_chain1(LdsChain1& c, const uint32_t* pay, const uint8_t* dtb, uint32_t p,
+                                              uint32_t p1, bool last, uint32_t n, uint8_t* __restrict__ out,
+                                              int32_t hdr_bits) {
+    constexpr uint32_t G = 2u * DEC_GROUP;  // 64 symbols = one 64-byte segment of output
+    for (; p + G <= p1; p += G) {
+        uint32_t w[G / 4u];
+#pragma unroll
+        for (uint32_t j = 0; j < G; j += 4u) {
+            const uint32_t e0 = c.step(pay, dtb), e1 = c.step(pay, dtb);
+            const uint32_t e2 = c.step(pay, dtb), e3 = c.step(pay, dtb);
+            w[j >> 2] = __builtin_amdgcn_perm(__builtin_amdgcn_perm(e3, e2, 0x0c0c0501u),
+                                              __builtin_amdgcn_perm(e1, e0, 0x0c0c0501u), 0x05040100u);
+        }
+        uint4* o4 = reinterpret_cast<uint4*>(out + p);
+#pragma unroll
+        for (uint32_t q = 0; q < G / 16u; ++q) o4[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+    }
+    for (; p < p1; ++p) out[p] = (uint8_t)dte_sym(c.step(pay, dtb));
+    // container mode: the raw length ends the block (as the 2-state path
+    // does); for a valid stream the reference's next read fails right here
+    if (last) out[n - 1u] = (uint8_t)dte_sym(*reinterpret_cast<const uint32_t*>(dtb + c.a));  // finish (lib.rs:208)
+    return FSE_OK;
+}
+
+// The same for blocks read from global memory (windowed reader).
+template <class RD>
+__device__ __forceinline__ int32_t decode_segment1(RD& br, uint32_t s, uint32_t p, uint32_t p1, bool last, uint32_t n,
+                                                   uint8_t* __restrict__ out, const uint32_t* dt, uint32_t smask,
+                                                   int32_t hdr_bits) {
+    for (; p < p1; ++p) {
+        const uint32_t e = dt[s & smask];
+        s = dte_ns(e) + br.pop(dte_nb(e));
+        br.refill();
+        out[p] = (uint8_t)dte_sym(e);
+    }
+    if (last) out[n - 1u] = (uint8_t)dte_sym(dt[s & smask]);
+    return FSE_OK;
+}
+
 template <int LMAX, uint32_t PMAX>
 struct PreSmem {
     uint32_t pay[PMAX / 4];
@@ -1166,7 +1270,7 @@ struct PreSmem {
     int err[16];
 };
 
-template <int LMAX, int NW, uint32_t PMAX, int VAR>
+template <int LMAX, int NW, uint32_t PMAX, int VAR, int NS = 2>
 __global__ __launch_bounds__(64 * NW) void decode_pre_kernel(DecParams P) {
     __shared__ PreSmem<LMAX, PMAX> sm;
     constexpr uint32_t NT = 64u * NW;
@@ -1223,14 +1327,35 @@ __global__ __launch_bounds__(64 * NW) void decode_pre_kernel(DecParams P) {
         return;
     }
     const uint32_t smask = (1u << L) - 1u;
-    const uint32_t Pm = (n & 1u) ? (n - 3u) / 2u : n / 2u - 1u;
+    // main-loop steps: pairs (NS = 2) or symbols below the last one (NS = 1)
+    const uint32_t Pm = NS == 2 ? ((n & 1u) ? (n - 3u) / 2u : n / 2u - 1u) : n - 1u;
     const uint32_t I = P.ckpt_interval;
     const uint32_t nseg = Pm / I + 1u;
     const uint64_t* sc = P.sidecar + gb * P.ckpt_per_block;
     const uint32_t maxbp = clen * 8u - (uint32_t)hdr_bits;
     const uint8_t* dtb = reinterpret_cast<const uint8_t*>(sm.dt);
     int32_t err = FSE_OK;
-    if (P.dual && in_lds) {  // two segments per lane: seg and seg + NT
+    if (NS == 1) {
+        for (uint32_t seg = tid; seg < nseg; seg += NT) {
+            const uint64_t e = sc[seg];
+            const uint32_t p0 = seg * I, p1 = min(p0 + I, Pm);
+            const uint32_t bp = (uint32_t)e, s0 = (uint32_t)(e >> 32) & smask;
+            const bool lastseg = seg == nseg - 1u;
+            int32_t r;
+            if (bp > maxbp) {
+                r = FSE_ERR_BAD_ARG;
+            } else if (in_lds && !PADDED) {
+                LdsChain1 c;
+                c.init(sm.pay, hdr_bits + (int32_t)bp, s0);
+                r = run_chain1(c, sm.pay, dtb, p0, p1, lastseg, n, out, hdr_bits);
+            } else {
+                GlobalReader br;
+                br.init(reinterpret_cast<const uint32_t*>(in), hdr_bits + (int32_t)bp);
+                r = decode_segment1(br, s0, p0, p1, lastseg, n, out, sm.dt, smask, hdr_bits);
+            }
+            if (r != FSE_OK) err = r;
+        }
+    } else if (P.dual && in_lds) {  // two segments per lane: seg and seg + NT
         for (uint32_t sa = tid; sa < nseg; sa += 2u * NT) {
             const uint32_t sb = sa + NT;
             const uint64_t ea = sc[sa];
@@ -1330,6 +1455,63 @@ __global__ __launch_bounds__(64) void dtable_blocks_kernel(DtParams P) {
         });
     }
     if (lane == 0) P.dtinfo[gb] = rc == FSE_OK ? (int32_t)((uint32_t)hl | (L << 16)) : rc;
+}
+
+// ------------------------------------------------------------------------
+// fse_decompress (lib.rs:187-211) in reference mode: no sidecar, raw length
+// unknown; one lane per block walks the stream with every read checked, on
+// tables from dtable_blocks_kernel.  Serial by nature (the host entry point
+// and streams produced elsewhere).
+// ------------------------------------------------------------------------
+template <int LMAX>
+__global__ __launch_bounds__(64) void decode1_serial_kernel(DecParams P) {
+    const uint64_t gb = blockIdx.x;
+    if (gb >= P.n_blocks || threadIdx.x != 0) return;
+    const int32_t info = P.dtinfo[gb];
+    if (info < 0) {
+        P.status[gb] = info;
+        if (P.out_len) P.out_len[gb] = 0;
+        return;
+    }
+    const uint8_t* in = P.in + gb * P.slot_bytes;
+    const uint32_t clen = P.comp_len[gb];
+    const int32_t hdr_bits = (info & 0xFFFF) * 8;
+    const uint32_t L = (uint32_t)info >> 16;
+    const uint32_t* dt = P.dt + gb * (uint64_t)(1u << LMAX);
+    uint8_t* out = P.out + gb * (uint64_t)P.block_size;
+    const bool known = P.n_total != 0;  // container length, else reference mode with a capacity
+    const uint32_t n = known ? (uint32_t)min((uint64_t)P.block_size, P.n_total - gb * (uint64_t)P.block_size) : 0u;
+    const uint32_t cap = known ? n : P.out_cap;
+    int32_t err = FSE_OK;
+    uint32_t o = 0;
+    const int32_t top = (int32_t)(clen - 1u) * 8 + (int32_t)ilog2u(in[clen - 1]);  // marker (BitStackReader::new)
+    GlobalReader br;
+    br.init(reinterpret_cast<const uint32_t*>(in), top);
+    if (br.pos - (int32_t)L < hdr_bits) {
+        err = FSE_ERR_TOO_SHORT;  // lib.rs:197 unwrap
+    } else {
+        uint32_t s = br.pop(L);
+        br.refill();
+        for (;;) {
+            const uint32_t e = dt[s];
+            const uint32_t nb = dte_nb(e);
+            if (br.pos - (int32_t)nb < hdr_bits) break;  // decode_symbol -> None
+            if (o >= cap) {  // nb == 0 forever: a probability-1 symbol never ends in the reference
+                err = nb == 0 ? FSE_ERR_SINGLE_SYMBOL : FSE_ERR_DST_TOO_SMALL;
+                break;
+            }
+            s = dte_ns(e) + br.pop(nb);
+            br.refill();
+            out[o++] = (uint8_t)dte_sym(e);
+        }
+        if (err == FSE_OK) {
+            if (o >= cap) err = FSE_ERR_DST_TOO_SMALL;
+            else out[o++] = (uint8_t)dte_sym(dt[s]);  // Decoder::finish (lib.rs:208)
+        }
+        if (known && (err == FSE_ERR_DST_TOO_SMALL || (err == FSE_OK && o != n))) err = FSE_ERR_LENGTH_MISMATCH;
+    }
+    P.status[gb] = err;
+    if (P.out_len) P.out_len[gb] = err ? 0u : o;
 }
 
 // ------------------------------------------------------------------------
@@ -1440,13 +1622,16 @@ __global__ __launch_bounds__(256) void generate_kernel(GenParams G) {
 hipError_t launch_encode(const EncParams& P, uint32_t lmax, hipStream_t stream) {
     const uint32_t T = P.lanes ? P.lanes : 64;
     const uint32_t bpw = 64u / T;
-    const uint32_t grid = (P.n_blocks + bpw - 1u) / bpw;
-    if (T == 64) {
-        if (lmax <= 11) hipLaunchKernelGGL((encode_blocks_kernel<11, 64>), dim3(grid), dim3(64), 0, stream, P);
-        else hipLaunchKernelGGL((encode_blocks_kernel<12, 64>), dim3(grid), dim3(64), 0, stream, P);
+    const dim3 g((P.n_blocks + bpw - 1u) / bpw), b(64);
+    if (P.nstates == 1) {  // fse_compress (lib.rs:112-143)
+        if (lmax <= 11) hipLaunchKernelGGL((encode_blocks_kernel<11, 64, 1>), g, b, 0, stream, P);
+        else hipLaunchKernelGGL((encode_blocks_kernel<12, 64, 1>), g, b, 0, stream, P);
+    } else if (T == 64) {
+        if (lmax <= 11) hipLaunchKernelGGL((encode_blocks_kernel<11, 64, 2>), g, b, 0, stream, P);
+        else hipLaunchKernelGGL((encode_blocks_kernel<12, 64, 2>), g, b, 0, stream, P);
     } else {
-        if (lmax <= 11) hipLaunchKernelGGL((encode_blocks_kernel<11, 32>), dim3(grid), dim3(64), 0, stream, P);
-        else hipLaunchKernelGGL((encode_blocks_kernel<12, 32>), dim3(grid), dim3(64), 0, stream, P);
+        if (lmax <= 11) hipLaunchKernelGGL((encode_blocks_kernel<11, 32, 2>), g, b, 0, stream, P);
+        else hipLaunchKernelGGL((encode_blocks_kernel<12, 32, 2>), g, b, 0, stream, P);
     }
     return hipGetLastError();
 }
@@ -1458,6 +1643,17 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
     if (P.dt) {  // prebuilt tables: lean kernel; LDS = image + table (44 KB image -> 3 WG/CU)
         constexpr uint32_t PP = 44u << 10;
         auto go = [&](auto kern, uint32_t threads) { hipLaunchKernelGGL(kern, g, dim3(threads), 0, stream, P); };
+        if (P.nstates == 1) {  // fse_decompress blocks: linear image, per-lane windows
+            if (!P.sidecar) {  // reference mode: serial, every read checked
+                if (lmax <= 11) go(decode1_serial_kernel<11>, 64);
+                else go(decode1_serial_kernel<12>, 64);
+            } else if (lmax <= 11) {
+                go(decode_pre_kernel<11, 4, PP, 2, 1>, 256);
+            } else {
+                go(decode_pre_kernel<12, 4, PP - 8192, 2, 1>, 256);
+            }
+            return hipGetLastError();
+        }
         if (P.waves == 8) {
             if (lmax <= 11) {
                 if (P.variant == 3) go(decode_pre_kernel<11, 8, PP, 3>, 512);

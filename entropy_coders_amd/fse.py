@@ -58,6 +58,30 @@ def decompress2(src, cap: int = 1 << 24) -> bytes:
     return dst[: n.value].tobytes()
 
 
+def compress(src) -> tuple[bytes, int]:
+    """`fse_compress(src, &mut dst) -> (NormHistogram, usize)` (lib.rs:112): the
+    1-state format; (bytes, payload bits).  The header in the bytes is the
+    returned NormHistogram."""
+    a = _buf(src)
+    lib = load()
+    cap = int(lib.fsehip_slot_bytes(max(len(a), 16), 12))
+    dst = np.zeros(cap, dtype=np.uint8)
+    n = C.c_size_t(0)
+    bits = C.c_uint64(0)
+    check(lib.fse_compress(_p(a), len(a), _p(dst), cap, C.byref(n), C.byref(bits)), "fse_compress")
+    return dst[: n.value].tobytes(), bits.value
+
+
+def decompress(src, cap: int = 1 << 24) -> bytes:
+    """`fse_decompress(src, &mut dst) -> Option<usize>` (lib.rs:187)."""
+    a = _buf(src)
+    lib = load()
+    dst = np.zeros(max(cap, 1), dtype=np.uint8)
+    n = C.c_size_t(0)
+    check(lib.fse_decompress(_p(a), len(a), _p(dst), cap, C.byref(n)), "fse_decompress")
+    return dst[: n.value].tobytes()
+
+
 def histogram_count(src) -> tuple[np.ndarray, int]:
     """`Histogram::new(data)` (histogram.rs:18-66): (counts[256], table_len)."""
     a = _buf(src)
@@ -77,7 +101,7 @@ class BlockCodec:
     """
 
     def __init__(self, block_size: int = 65536, table_log: int = 0, ckpt_interval: int = 128,
-                 device=None):
+                 device=None, nstates: int = 2):
         import torch
 
         self.torch = torch
@@ -85,13 +109,14 @@ class BlockCodec:
         self.block_size = block_size
         self.table_log = table_log
         self.ckpt_interval = ckpt_interval
+        self.nstates = nstates  # 2: fse_compress2 blocks (lib.rs:146), 1: fse_compress (lib.rs:112)
         self.max_table_log = max(11, table_log) if table_log else 11
         self.lib = load()
         self.slot_bytes = int(self.lib.fsehip_slot_bytes(block_size, self.max_table_log))
-        self.side_per_block = int(self.lib.fsehip_sidecar_per_block(block_size, ckpt_interval))
+        self.side_per_block = int(self.lib.fsehip_sidecar_per_block_ns(block_size, ckpt_interval, nstates))
 
     def params(self) -> Params:
-        return Params(self.block_size, self.table_log, self.ckpt_interval, self.max_table_log)
+        return Params(self.block_size, self.table_log, self.ckpt_interval, self.max_table_log, self.nstates)
 
     def _stream(self):
         return C.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
@@ -160,12 +185,14 @@ class BlockCodec:
             self.n_blocks(cb["n_total"]), C.c_void_p(tabs["dt"].data_ptr()), C.c_void_p(tabs["info"].data_ptr()),
             self._stream()), "fsehip_build_dtables")
 
-    def decompress_dt_into(self, cb: dict, tabs: dict, out, status) -> None:
-        """Decode with pre-built tables (needs the sidecar)."""
+    def decompress_dt_into(self, cb: dict, tabs: dict, out, status, use_sidecar: bool = True) -> None:
+        """Decode with pre-built tables (2-state needs the sidecar; 1-state
+        without one runs the serial reference-order decoder)."""
         p = self.params()
+        side = C.c_void_p(cb["sidecar"].data_ptr()) if (use_sidecar and self.ckpt_interval) else None
         check(self.lib.fsehip_decompress_blocks_dt(
             C.byref(p), C.c_void_p(cb["out"].data_ptr()), self.slot_bytes, C.c_void_p(cb["comp_len"].data_ptr()),
-            C.c_void_p(cb["sidecar"].data_ptr()), C.c_void_p(tabs["dt"].data_ptr()),
+            side, C.c_void_p(tabs["dt"].data_ptr()),
             C.c_void_p(tabs["info"].data_ptr()), C.c_void_p(out.data_ptr()), cb["n_total"],
             C.c_void_p(status.data_ptr()), self._stream()), "fsehip_decompress_blocks_dt")
 
@@ -183,4 +210,5 @@ class BlockCodec:
         return cb["out"][s: s + ln].cpu().numpy().tobytes()
 
 
-__all__ = ["BlockCodec", "FseError", "compress2", "compress2_log", "decompress2", "histogram_count"]
+__all__ = ["BlockCodec", "FseError", "compress", "compress2", "compress2_log", "decompress", "decompress2",
+           "histogram_count"]

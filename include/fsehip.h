@@ -56,6 +56,13 @@ int fse_compress2_log(const uint8_t* src, size_t n, uint32_t table_log, uint8_t*
  * case -> SINGLE_SYMBOL. */
 int fse_decompress2(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, size_t* dst_len);
 
+/* The 1-state format: replaces `pub fn fse_compress(src, dst) -> (NormHistogram, usize)`
+ * (lib.rs:112; the returned NormHistogram is the block's own header) and
+ * `pub fn fse_decompress(src, dst) -> Option<usize>` (lib.rs:187), same
+ * conventions as the 2-state pair above. */
+int fse_compress(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, size_t* dst_len, uint64_t* payload_bits);
+int fse_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, size_t* dst_len);
+
 /* Replaces `Histogram::new(data)` (histogram.rs:18-66) -- the north star's
  * `histogram::count`: counts[256], table_len = 1 + largest symbol. */
 int histogram_count(const uint8_t* src, size_t n, uint32_t counts[256], uint32_t* table_len);
@@ -67,14 +74,18 @@ int histogram_count(const uint8_t* src, size_t n, uint32_t counts[256], uint32_t
 typedef struct {
     uint32_t block_size;    /* bytes per block; multiple of 16 when >1 block; default 65536 */
     uint32_t table_log;     /* 0 = NormHistogram::new (optimal); else Histogram::normalize(L) */
-    uint32_t ckpt_interval; /* pairs between decode checkpoints (power of two >= 8), 0 = none */
+    uint32_t ckpt_interval; /* steps between decode checkpoints (power of two; >= 8 for 2-state
+                               pairs, >= 16 for 1-state symbols), 0 = none */
     uint32_t max_table_log; /* upper bound on L used by the blocks (11 or 12); 0 = derive */
+    uint32_t nstates;       /* block format: 2 (or 0) = fse_compress2 (lib.rs:146), 1 = fse_compress (lib.rs:112) */
 } fsehip_params;
 
 /* Per-block output slot size (bytes) able to hold any block of block_size
- * bytes at tableLog <= max_table_log, and sidecar entries per block. */
+ * bytes at tableLog <= max_table_log, and sidecar entries per block (2-state
+ * blocks; the _ns variant covers both formats). */
 uint64_t fsehip_slot_bytes(uint32_t block_size, uint32_t max_table_log);
 uint32_t fsehip_sidecar_per_block(uint32_t block_size, uint32_t ckpt_interval);
+uint32_t fsehip_sidecar_per_block_ns(uint32_t block_size, uint32_t ckpt_interval, uint32_t nstates);
 
 /* Compress n_total bytes as ceil(n_total/block_size) independent blocks.
  * Block b's bytes go to d_out + b*slot_bytes (comp_len[b] bytes, exactly

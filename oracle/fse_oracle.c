@@ -770,6 +770,37 @@ int fo_checkpoints2(const uint8_t* src, size_t n, uint32_t interval, uint32_t* b
     return FSE_OK;
 }
 
+/* Decode checkpoints of a 1-state (fse_compress) stream: the state just
+ * before it decodes symbol p (lib.rs:197-207), every `interval` symbols.    */
+int fo_checkpoints1(const uint8_t* src, size_t n, uint32_t interval, uint32_t* bitpos, uint16_t* s0o,
+                    size_t cap, size_t* count) {
+    fo_norm nh;
+    size_t hlen;
+    int rc = fo_header_read(src, n, &nh, &hlen);
+    if (rc) return rc;
+    sr_t r;
+    rc = sr_init(&r, src + hlen, n - hlen);
+    if (rc) return rc;
+    static __thread fo_dtable dt;
+    rc = fo_build_dtable(&nh, &dt);
+    if (rc) return rc;
+    uint32_t st;
+    if (!sr_pop(&r, nh.log2, &st)) return FSE_ERR_TOO_SHORT;
+    size_t c = 0;
+    for (uint64_t p = 0;; ++p) {
+        if (interval && p % interval == 0) {
+            if (c >= cap) return FSE_ERR_DST_TOO_SMALL;
+            bitpos[c] = (uint32_t)r.top;
+            s0o[c] = (uint16_t)st;
+            c++;
+        }
+        uint8_t sym;
+        if (!dec_step(&dt, &st, &r, &sym)) break;
+    }
+    *count = c;
+    return FSE_OK;
+}
+
 /* ======================================================================
  * Bitstream property helpers (bitstream/mod.rs:29-110)
  * ====================================================================== */

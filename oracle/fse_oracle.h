@@ -111,6 +111,9 @@ int fo_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap,
 int fo_checkpoints2(const uint8_t* src, size_t n, uint32_t interval,
                     uint32_t* bitpos, uint16_t* s0, uint16_t* s1, size_t cap,
                     size_t* count);
+/* The same for a 1-state stream: the state before symbol p.              */
+int fo_checkpoints1(const uint8_t* src, size_t n, uint32_t interval, uint32_t* bitpos, uint16_t* s0o,
+                    size_t cap, size_t* count);
 
 /* ---- bitstream primitives (bitstream/ files), for property tests ---- */
 /* Write (val,bits) pairs LSB-first after `offset` pre-existing bytes, then

@@ -81,6 +81,7 @@ def lib():
         _lib.fo_build_ctable.argtypes = [C.POINTER(Norm), C.POINTER(CTable)]
         _lib.fo_build_dtable.argtypes = [C.POINTER(Norm), C.POINTER(DTable)]
         _lib.fo_checkpoints2.argtypes = [P, sz, C.c_uint32, P, P, P, sz, C.POINTER(sz)]
+        _lib.fo_checkpoints1.argtypes = [P, sz, C.c_uint32, P, P, sz, C.POINTER(sz)]
         _lib.fo_bits_write.argtypes = [P, P, sz, C.c_int, P, sz, C.POINTER(C.c_uint64)]
         _lib.fo_bits_write.restype = sz
         _lib.fo_bits_read_stack.argtypes = [P, sz, P, sz, P, C.POINTER(sz)]
@@ -202,6 +203,17 @@ def dtable(data):
     size = 1 << dt.log2
     return (dt.log2, np.ctypeslib.as_array(dt.new_state)[:size].copy(),
             np.ctypeslib.as_array(dt.sym)[:size].copy(), np.ctypeslib.as_array(dt.nb)[:size].copy(), used)
+
+
+def checkpoints1(data, interval: int):
+    """1-state decode checkpoints: (bitpos, state) before symbol p, every interval."""
+    a = _u8(data)
+    cap = 1 << 20
+    bp = np.zeros(cap, np.uint32)
+    s0 = np.zeros(cap, np.uint16)
+    cnt = C.c_size_t(0)
+    _check(lib().fo_checkpoints1(_ptr(a), len(a), interval, _ptr(bp), _ptr(s0), cap, C.byref(cnt)))
+    return bp[: cnt.value], s0[: cnt.value]
 
 
 def checkpoints2(data, interval: int):

@@ -195,3 +195,15 @@ def test_checkpoints_consistent():
     bp, s0, s1 = O.checkpoints2(comp, 512)
     assert len(bp) == 64
     assert bp[0] > bp[-1]  # decoding walks the stack downward
+
+
+def test_checkpoints1_consistent():
+    """1-state checkpoints: one per `interval` symbols of the n-1 decoded by
+    the loop plus the one before the final state symbol when it lands on the
+    grid; the first holds the seed state popped first (lib.rs:197)."""
+    for n, iv in [(65536, 512), (5000, 16), (4097, 64)]:
+        src = O.generate(1, 0.5, 4, 1, n)
+        comp, _ = O.compress(src)
+        bp, s0 = O.checkpoints1(comp, iv)
+        assert len(bp) == (n - 1) // iv + 1
+        assert np.all(np.diff(bp.astype(np.int64)) < 0)
