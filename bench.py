@@ -37,6 +37,8 @@ def parse():
     ap.add_argument("--kind", type=int, default=0)
     ap.add_argument("--table-log", type=int, default=0)
     ap.add_argument("--ckpt", type=int, default=128)
+    ap.add_argument("--nstates", type=int, default=2, choices=(1, 2),
+                    help="block format: 2 = fse_compress2 (the headline), 1 = fse_compress")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-c3", action="store_true", help="skip the decode-only (prebuilt tables) line")
@@ -125,7 +127,7 @@ def main():
     from entropy_coders_amd import BlockCodec
 
     codec = BlockCodec(block_size=args.block, table_log=args.table_log, ckpt_interval=args.ckpt,
-                       device=dev)
+                       device=dev, nstates=args.nstates)
     n = args.bytes
     seed = 0x5EED0002 ^ (rank * 0x1000193)
     src = codec.generate(args.kind, args.prob, seed, n)
@@ -170,8 +172,10 @@ def main():
           and bool(torch.equal(out, src)))
     comp_bytes = int(cb["comp_len"].to(torch.int64).sum())
     nb = codec.n_blocks(n)
-    side_bytes = 8 * sum(n_ck for n_ck in [((min(args.block, n - b * args.block) // 2) // args.ckpt + 1)
-                                           for b in range(nb)]) if args.ckpt else 0
+    def n_ckpt(ln):  # sidecar entries of a block of ln bytes (pairs for 2-state, symbols for 1-state)
+        return (ln // 2) // args.ckpt + 1 if args.nstates == 2 else (ln - 1) // args.ckpt + 1
+
+    side_bytes = 8 * sum(n_ckpt(min(args.block, n - b * args.block)) for b in range(nb)) if args.ckpt else 0
     if world > 1:
         flag = torch.tensor([1 if ok else 0], device=dev)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
@@ -250,10 +254,12 @@ def main():
             "data": "synthetic",
             "config": {
                 "workload": "C2: 1 GiB per GPU as 16384 x 64 KiB independent blocks, LUT generator "
-                            f"p={args.prob} (H~4.02 bits/sym), encode (fse_compress2-exact) + decode",
+                            f"p={args.prob} (H~4.02 bits/sym), encode "
+                            f"({'fse_compress2' if args.nstates == 2 else 'fse_compress'}-exact) + decode",
+                "format": "2-state (fse_compress2)" if args.nstates == 2 else "1-state (fse_compress)",
                 "block_size": args.block,
                 "table_log": args.table_log or "optimal (11)",
-                "ckpt_interval_pairs": args.ckpt,
+                "ckpt_interval": f"{args.ckpt} {'pairs' if args.nstates == 2 else 'symbols'}",
                 "parallelism": f"dp{world} (blocks sharded per GPU, no collective in the step)",
             },
             "roofline": {

@@ -91,17 +91,39 @@ struct Stamps {
         (void)hipStreamSynchronize(s);
         std::vector<uint64_t> h(groups * fsehip::kStamps);
         (void)hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost);
-        double acc[fsehip::kStamps] = {0};
-        size_t cnt[fsehip::kStamps] = {0};
-        for (size_t g = 0; g < groups; ++g)
-            for (int k = 1; k < fsehip::kStamps; ++k) {
-                const uint64_t a = h[g * fsehip::kStamps + k - 1], b = h[g * fsehip::kStamps + k];
-                if (a && b && b >= a) { acc[k] += (double)(b - a); cnt[k]++; }
+        // deltas between consecutive recorded slots (kernels may skip slots);
+        // per XCD (workgroups are placed round-robin over the 8 XCDs) the
+        // span from the first start to the last stamp, for the mean number
+        // of workgroups in flight per CU (32 CUs per XCD)
+        double acc[fsehip::kStamps] = {0}, life = 0;
+        size_t cnt[fsehip::kStamps] = {0}, nlife = 0;
+        uint64_t lo_x[8], hi_x[8];
+        for (int x = 0; x < 8; ++x) lo_x[x] = ~0ull, hi_x[x] = 0;
+        for (size_t g = 0; g < groups; ++g) {
+            const uint64_t* r = &h[g * fsehip::kStamps];
+            int prev = -1;
+            for (int k = 0; k < fsehip::kStamps - 1; ++k) {
+                if (!r[k]) continue;
+                if (prev >= 0 && r[k] >= r[prev]) { acc[k] += (double)(r[k] - r[prev]); cnt[k]++; }
+                prev = k;
             }
+            if (r[0] && prev > 0 && r[prev] >= r[0]) {
+                life += (double)(r[prev] - r[0]);
+                nlife++;
+                lo_x[g % 8] = std::min(lo_x[g % 8], r[0]);
+                hi_x[g % 8] = std::max(hi_x[g % 8], r[prev]);
+            }
+        }
         fprintf(stderr, "[stamps] %s:", what);
         for (int k = 1; k < fsehip::kStamps - 1; ++k)
             if (cnt[k]) fprintf(stderr, " %d:%.0f", k, acc[k] / cnt[k]);
-        fprintf(stderr, " (mean cycles per workgroup between stamps k-1 and k)\n");
+        double span = 0;
+        for (int x = 0; x < 8; ++x)
+            if (hi_x[x] > lo_x[x]) span += (double)(hi_x[x] - lo_x[x]);
+        fprintf(stderr, " (mean cycles per workgroup since the previous stamp)\n");
+        if (nlife && span > 0)
+            fprintf(stderr, "[stamps] %s: lifetime %.0f cycles, XCD span %.0f cycles, %.2f workgroups in flight per CU\n",
+                    what, life / nlife, span / 8, life / (span * 32.0) * ((double)groups / nlife));
         // slot kStamps-1: kernel-defined counters (low / high 32 bits), averaged
         double lo = 0, hi = 0;
         for (size_t g = 0; g < groups; ++g) {
@@ -306,6 +328,7 @@ static int decompress_impl(const fsehip_params* p, const uint8_t* d_in, uint64_t
     P.waves = env_u32("FSEHIP_DEC_WAVES", 4) == 8 ? 8 : 4;
     P.variant = env_u32("FSEHIP_DEC_VAR", 2);
     P.dual = env_u32("FSEHIP_DEC_DUAL", 0);
+    P.stage_kib = env_u32("FSEHIP_DEC_PP", 44);
     // the decoder reads L from each header; size its tables for the bound
     uint32_t lmax = p->max_table_log ? p->max_table_log : 12;
     P.dt = d_dt;
@@ -543,6 +566,12 @@ int histogram_count(const uint8_t* src, size_t n, uint32_t counts[256], uint32_t
     memcpy(counts, h, 256 * sizeof(uint32_t));
     if (table_len) *table_len = h[256];
     return FSE_OK;
+}
+
+// Diagnostics only (not part of include/fsehip.h): resident workgroups per CU.
+int fsehipx_occupancy(char* buf, int cap) {
+    if (!buf || cap <= 0 || !device_ok()) return 0;
+    return fsehip::occupancy_report(buf, cap);
 }
 
 }  // extern "C"

@@ -48,6 +48,7 @@ struct DecParams {
     const int32_t* dtinfo;  // per block: header bytes | L << 16, or < 0 = status
     uint32_t variant;       // LDS layout / reader: 3/5 = padded image (prebuilt tables), else linear window
     uint32_t dual;          // two segments per lane, interleaved (prebuilt-table kernel)
+    uint32_t stage_kib;     // LDS image size of the prebuilt-table kernel: 44 (default), 40 or 36 KiB
     uint32_t nstates;       // 2 = fse_compress2 blocks (default), 1 = fse_compress blocks
 };
 
@@ -76,6 +77,8 @@ constexpr int kStamps = 10;  // stamp slots per workgroup
 hipError_t launch_encode(const EncParams& P, uint32_t lmax, hipStream_t stream);
 hipError_t launch_dtables(const DtParams& P, uint32_t lmax, hipStream_t stream);
 hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream);
+// Diagnostics: resident workgroups per CU of the main kernels, as text.
+int occupancy_report(char* buf, int cap);
 hipError_t launch_histogram(const uint8_t* src, uint64_t n_total, uint32_t block_size, uint32_t n_blocks,
                             uint32_t* counts, uint32_t* table_len, hipStream_t stream);
 hipError_t launch_generate(const GenParams& G, hipStream_t stream);

@@ -1270,7 +1270,7 @@ struct PreSmem {
     int err[16];
 };
 
-template <int LMAX, int NW, uint32_t PMAX, int VAR, int NS = 2>
+template <int LMAX, int NW, uint32_t PMAX, int VAR, int NS = 2, bool DUAL = false>
 __global__ __launch_bounds__(64 * NW) void decode_pre_kernel(DecParams P) {
     __shared__ PreSmem<LMAX, PMAX> sm;
     constexpr uint32_t NT = 64u * NW;
@@ -1355,7 +1355,8 @@ __global__ __launch_bounds__(64 * NW) void decode_pre_kernel(DecParams P) {
             }
             if (r != FSE_OK) err = r;
         }
-    } else if (P.dual && in_lds) {  // two segments per lane: seg and seg + NT
+    } else if (DUAL && in_lds) {  // two segments per lane: seg and seg + NT (own instantiation: its
+                                  // two chains would otherwise set the kernel's VGPR count)
         for (uint32_t sa = tid; sa < nseg; sa += 2u * NT) {
             const uint32_t sb = sa + NT;
             const uint64_t ea = sc[sa];
@@ -1666,8 +1667,14 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
             }
         } else {
             if (lmax <= 11) {
-                if (P.variant == 3) go(decode_pre_kernel<11, 4, PP, 3>, 256);
+                if (P.dual) {
+                    if (P.variant == 3) go(decode_pre_kernel<11, 4, PP, 3, 2, true>, 256);
+                    else if (P.variant == 5) go(decode_pre_kernel<11, 4, PP, 5, 2, true>, 256);
+                    else go(decode_pre_kernel<11, 4, PP, 2, 2, true>, 256);
+                } else if (P.variant == 3) go(decode_pre_kernel<11, 4, PP, 3>, 256);
                 else if (P.variant == 5) go(decode_pre_kernel<11, 4, PP, 5>, 256);
+                else if (P.stage_kib == 40) go(decode_pre_kernel<11, 4, (40u << 10), 2>, 256);
+                else if (P.stage_kib == 36) go(decode_pre_kernel<11, 4, (36u << 10), 2>, 256);
                 else go(decode_pre_kernel<11, 4, PP, 2>, 256);
             } else {
                 if (P.variant == 3) go(decode_pre_kernel<12, 4, PP - 8192, 3>, 256);
@@ -1685,6 +1692,28 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
         else hipLaunchKernelGGL((decode_blocks_kernel<12, 4, PM4>), g, dim3(256), 0, stream, P);
     }
     return hipGetLastError();
+}
+
+int occupancy_report(char* buf, int cap) {
+    int len = 0;
+    auto one = [&](const char* name, const void* k, int threads) {
+        int nb = -1;
+        hipFuncAttributes fa{};
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, threads, 0);
+        (void)hipFuncGetAttributes(&fa, k);
+        if (len < cap)
+            len += snprintf(buf + len, cap - len, "%s: %d WG/CU (lds %zu B, vgpr %d)\n", name, nb,
+                            fa.sharedSizeBytes, fa.numRegs);
+    };
+    one("encode<11,64,2>", reinterpret_cast<const void*>(encode_blocks_kernel<11, 64, 2>), 64);
+    one("dtable<11>", reinterpret_cast<const void*>(dtable_blocks_kernel<11>), 64);
+    one("decode_pre<11,4,44K,2>", reinterpret_cast<const void*>(decode_pre_kernel<11, 4, (44u << 10), 2>), 256);
+    one("decode_pre<11,4,40K,2>", reinterpret_cast<const void*>(decode_pre_kernel<11, 4, (40u << 10), 2>), 256);
+    one("decode_pre<11,4,36K,2>", reinterpret_cast<const void*>(decode_pre_kernel<11, 4, (36u << 10), 2>), 256);
+    one("decode_pre<11,4,44K,3>", reinterpret_cast<const void*>(decode_pre_kernel<11, 4, (44u << 10), 3>), 256);
+    one("decode_pre<11,8,44K,3>", reinterpret_cast<const void*>(decode_pre_kernel<11, 8, (44u << 10), 3>), 512);
+    one("decode_blocks<11,4>", reinterpret_cast<const void*>(decode_blocks_kernel<11, 4, (39u << 10)>), 256);
+    return len;
 }
 
 hipError_t launch_dtables(const DtParams& P, uint32_t lmax, hipStream_t stream) {

@@ -16,13 +16,13 @@ def main():
     n = int(os.environ.get("ABL_BYTES", 1 << 30))
     kind = int(os.environ.get("ABL_KIND", 0))
     prob = float(os.environ.get("ABL_PROB", 0.155))
-    for ckpt in (64,):
+    for ckpt in (int(os.environ.get("ABL_CKPT", 64)),):
         codec = BlockCodec(ckpt_interval=ckpt)
         src = codec.generate(kind, prob, 0x5EED0002, n)
         cb = codec.compress(src)
         out = torch.empty(n, dtype=torch.uint8, device="cuda")
         st = torch.zeros(codec.n_blocks(n), dtype=torch.int32, device="cuda")
-        for waves, var, dual in ((4, 2, 0), (4, 3, 0), (4, 3, 1), (4, 5, 1), (4, 2, 1), (8, 3, 0)):
+        for waves, var, dual in ((4, 2, 0), (4, 3, 0), (4, 5, 0), (4, 3, 1), (4, 5, 1), (8, 2, 0), (8, 3, 0), (8, 5, 0)):
             os.environ["FSEHIP_DEC_WAVES"] = str(waves)
             os.environ["FSEHIP_DEC_VAR"] = str(var)
             os.environ["FSEHIP_DEC_DUAL"] = str(dual)

@@ -13,8 +13,6 @@ while read -r SET; do
 done <<SETS
 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS
 SQ_LEVEL_WAVES SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU
-FETCH_SIZE
-WRITE_SIZE
-GRBM_GUI_ACTIVE GRBM_COUNT
+GRBM_GUI_ACTIVE GRBM_COUNT SQ_WAIT_INST_LDS SQ_INST_LEVEL_LDS SQ_LDS_ADDR_CONFLICT SQ_ACTIVE_INST_SCA SQ_INSTS_SMEM
 SETS
 echo done

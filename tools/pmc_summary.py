@@ -12,7 +12,9 @@ import json
 import sys
 from collections import defaultdict
 
-KERNELS = {"encode_blocks_kernel": "fse_encode_blocks", "decode_blocks_kernel": "fse_decode_blocks",
+KERNELS = {"encode_blocks_kernel": "fse_encode_blocks", "decode_blocks_kernel": "fse_decode_blocks_fused",
+           "decode_pre_kernel": "fse_decode_blocks", "dtable_blocks_kernel": "fse_build_dtables",
+           "decode1_serial_kernel": "fse_decode1_serial",
            "pack_blocks_kernel": "fse_pack_blocks", "generate_kernel": "fse_generate"}
 
 

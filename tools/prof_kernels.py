@@ -10,7 +10,7 @@ import torch  # noqa: E402
 from entropy_coders_amd import BlockCodec  # noqa: E402
 
 n = int(os.environ.get("PROF_BYTES", 1 << 30))
-codec = BlockCodec()
+codec = BlockCodec(nstates=int(os.environ.get("PROF_NSTATES", 2)))
 src = codec.generate(0, 0.155, 0x5EED0002, n)
 cb = codec.alloc(n)
 out = torch.empty(n, dtype=torch.uint8, device="cuda")
