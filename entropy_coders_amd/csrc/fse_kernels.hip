@@ -321,25 +321,32 @@ struct EncSmem {
     uint16_t st[BPW][SIZE];
     uint2 tt[BPW][256];
     uint32_t hdrw[BPW][HDR_MAX / 4];
+    // phase-1 scratch (statistics, header, spread) and phase-2 scratch
+    // (trajectories, end states, merge list) share the same LDS: 13.4 KB per
+    // workgroup at L <= 11, so 12 workgroups fit a CU (the VGPR limit)
     union {
-        uint32_t hs[HIST_WORDS];
         struct {
-            uint8_t sym_at[SIZE];
-            uint8_t occ_sym[SIZE];
-        } sp;
-        uint2 cp[64 * 8];  // phase 2: count-pass trajectories (Track), 8 slots per lane
-    } tmp;
-    uint32_t counts[256];
-    int32_t norm[256];
-    uint16_t cumul[256];
-    uint32_t cnt[256];
+            union {
+                uint32_t hs[HIST_WORDS];  // sub-histograms; counts[] = hs[0..255] after the reduction
+                struct {
+                    uint8_t sym_at[SIZE];
+                    uint8_t occ_sym[SIZE];
+                } sp;
+            } u;
+            int32_t norm[256];
+            uint16_t cumul[256];
+            uint32_t cnt[256];
+        } p1;
+        struct {
+            uint2 cp[64 * 8];  // count-pass trajectories (Track), 8 slots per lane
+            uint32_t cntF[BPW][T + 1];
+            uint32_t mword[BPW][2 * (T + 1)];
+            uint32_t mval[BPW][2 * (T + 1)];
+        } p2;
+    } ph;
     int32_t info_status[BPW];
     uint32_t info_L[BPW];
     uint32_t info_hl[BPW];
-    uint32_t specF[BPW][T + 1];
-    uint32_t cntF[BPW][T + 1];
-    uint32_t mword[BPW][2 * (T + 1)];
-    uint32_t mval[BPW][2 * (T + 1)];
     int scratch[4];
 };
 
@@ -360,18 +367,18 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
         const uint64_t off = gb * P.block_size;
         const uint32_t n = (uint32_t)min((uint64_t)P.block_size, P.n_total - off);
         const uint8_t* blk = P.src + off;
-        const uint32_t tl = wave_histogram(blk, n, sm.tmp.hs, sm.counts);
+        const uint32_t tl = wave_histogram(blk, n, sm.ph.p1.u.hs, sm.ph.p1.u.hs);
         FSE_STAMP(P, 1);
         int rc = FSE_OK;
         uint32_t Lreq = P.table_log, L = 0, slow = 0;
         if (n == 0) rc = FSE_ERR_EMPTY;
         if (rc == FSE_OK && P.table_log == 0) rc = optimal_log2(n, tl, &Lreq);  // histogram.rs:301
-        if (rc == FSE_OK) rc = wave_normalize(sm.counts, n, tl, Lreq, sm.norm, &L, &slow, sm.scratch);
+        if (rc == FSE_OK) rc = wave_normalize(sm.ph.p1.u.hs, n, tl, Lreq, sm.ph.p1.norm, &L, &slow, sm.scratch);
         if (rc == FSE_OK && n < 2) rc = FSE_ERR_TOO_SHORT;  // lib.rs:154/156 unwrap
         if (rc == FSE_OK && L > (uint32_t)LMAX) rc = FSE_ERR_UNSUPPORTED;
         FSE_STAMP(P, 2);
         if (rc == FSE_OK) {
-            const int hl = wave_header_write(sm.norm, L, tl, sm.hdrw[b]);
+            const int hl = wave_header_write(sm.ph.p1.norm, L, tl, sm.hdrw[b]);
             if (lane == 0) sm.scratch[1] = hl;
             if (hl < 0) rc = hl;
         }
@@ -379,17 +386,17 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
         if (rc == FSE_OK) {
             const uint32_t size = 1u << L;
             uint16_t* st = sm.st[b];
-            const uint16_t* cumul = sm.cumul;
-            rc = wave_build_spread(sm.norm, L, tl, sm.tmp.sp.sym_at, sm.tmp.sp.occ_sym, sm.cumul, sm.cnt,
+            const uint16_t* cumul = sm.ph.p1.cumul;
+            rc = wave_build_spread(sm.ph.p1.norm, L, tl, sm.ph.p1.u.sp.sym_at, sm.ph.p1.u.sp.occ_sym, sm.ph.p1.cumul, sm.ph.p1.cnt,
                                    [&](uint32_t i, uint32_t s, uint32_t r) {
                                        st[cumul[s] + r] = (uint16_t)(size + i);  // fse.rs:157-162
                                    });
             // symbol transforms, fse.rs:165-188 (total == cumul[s])
             for (uint32_t s = lane; s < 256; s += WAVE) {
-                int32_t x = (s < tl) ? sm.norm[s] : 0;
+                int32_t x = (s < tl) ? sm.ph.p1.norm[s] : 0;
                 uint2 t = make_uint2(0, 0);
                 if (s < tl) {
-                    const int32_t tot = (int32_t)sm.cumul[s];
+                    const int32_t tot = (int32_t)sm.ph.p1.cumul[s];
                     if (x == 0) {
                         t.x = ((L + 1u) << 16) - (1u << L);
                     } else if (x == -1 || x == 1) {
@@ -445,7 +452,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     // odd-length extra step), every other lane from a guessed start state,
     // recording its trajectory.  Then verify against the neighbour's end
     // state and repair by convergence (Track) until the fixed point.
-    Track tr{&sm.tmp.cp[lane * 8u], max(1u, (S / SPC + 7u) / 8u), false, 0u};
+    Track tr{&sm.ph.p2.cp[lane * 8u], max(1u, (S / SPC + 7u) / 8u), false, 0u};
     const uint32_t nslot = pb > pa ? (((pb - 1u) / SPC) - (pa / SPC)) / tr.ckc + 1u : 0u;
     uint32_t start = (1u << L) | (NS == 2 ? (1u << L) << 16 : 0u);
     uint32_t bits = 0;
@@ -453,7 +460,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
         EncState e0 = (k == ktop) ? top_start<PASS_COUNT, NS>(blk, n, tab, em) : EncState{start & 0xFFFFu, start >> 16, 0u};
         e0 = enc_range<PASS_COUNT, NS>(blk, n, pa, pb, e0, tab, em, ck, tr);
         bits = e0.bits;
-        sm.cntF[b][k] = e0.x0 | (e0.x1 << 16);
+        sm.ph.p2.cntF[b][k] = e0.x0 | (e0.x1 << 16);
         track_fixup(tr, nslot, -1, bits);
     }
     FSE_STAMP(P, 5);
@@ -463,7 +470,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
         bool bad = false;
         uint32_t nbF = 0;
         if (act && k < ktop) {
-            nbF = sm.cntF[b][k + 1];
+            nbF = sm.ph.p2.cntF[b][k + 1];
             bad = nbF != start;
         }
         __syncthreads();
@@ -476,7 +483,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
             const EncState e0 = enc_range<PASS_REPAIR, NS>(blk, n, pa, pb, EncState{start & 0xFFFFu, start >> 16, 0u},
                                                        tab, em, ck, tr);
             bits = e0.bits;
-            if (!tr.done) sm.cntF[b][k] = e0.x0 | (e0.x1 << 16);  // did not converge: new end state
+            if (!tr.done) sm.ph.p2.cntF[b][k] = e0.x0 | (e0.x1 << 16);  // did not converge: new end state
             track_fixup(tr, nslot, tr.done ? (int32_t)tr.jstar : -1, bits);
         }
     }
@@ -502,7 +509,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
 
     // emit pass
     for (uint32_t e = k; e < 2u * (T + 1u); e += T) {
-        if (b < BPW) sm.mword[b][e] = 0xFFFFFFFFu;
+        if (b < BPW) sm.ph.p2.mword[b][e] = 0xFFFFFFFFu;
     }
     __syncthreads();
     if (act && fits) {
@@ -537,12 +544,12 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
         // boundary words -> merge list (entry order = stream order)
         const uint32_t slot = 2u * (T - k);
         if ((off & 31u) != 0u && em.word > em.w0) {  // first word stored with the low bits empty
-            sm.mword[b][slot] = em.w0;
-            sm.mval[b][slot] = em.head_val;
+            sm.ph.p2.mword[b][slot] = em.w0;
+            sm.ph.p2.mval[b][slot] = em.head_val;
         }
         if (em.nacc) {  // last word never stored
-            sm.mword[b][slot + 1] = em.word;
-            sm.mval[b][slot + 1] = (uint32_t)em.acc;
+            sm.ph.p2.mword[b][slot + 1] = em.word;
+            sm.ph.p2.mval[b][slot + 1] = (uint32_t)em.acc;
         }
     }
     // header: whole words stored directly, the last partial word merged
@@ -554,8 +561,8 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
         if (k == 0 && (hl & 3u)) {
             uint32_t v = 0;
             for (uint32_t i = hl & ~3u; i < hl; ++i) v |= (uint32_t)h[i] << (8u * (i & 3u));
-            sm.mword[b][0] = hl / 4u;
-            sm.mval[b][0] = v;
+            sm.ph.p2.mword[b][0] = hl / 4u;
+            sm.ph.p2.mval[b][0] = v;
         }
     }
     FSE_STAMP(P, 7);
@@ -565,22 +572,22 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     if (live && fits) {
         constexpr uint32_t NE = 2u * (T + 1u);
         for (uint32_t e = k; e < NE; e += T) {
-            const uint32_t w = sm.mword[b][e];
+            const uint32_t w = sm.ph.p2.mword[b][e];
             if (w == 0xFFFFFFFFu) continue;
             bool first = true;
             for (int q = (int)e - 1; q >= 0; --q) {
-                const uint32_t wq = sm.mword[b][q];
+                const uint32_t wq = sm.ph.p2.mword[b][q];
                 if (wq == 0xFFFFFFFFu) continue;
                 first = (wq != w);
                 break;
             }
             if (!first) continue;
-            uint32_t v = sm.mval[b][e];
+            uint32_t v = sm.ph.p2.mval[b][e];
             for (uint32_t q = e + 1; q < NE; ++q) {
-                const uint32_t wq = sm.mword[b][q];
+                const uint32_t wq = sm.ph.p2.mword[b][q];
                 if (wq == 0xFFFFFFFFu) continue;
                 if (wq != w) break;
-                v |= sm.mval[b][q];
+                v |= sm.ph.p2.mval[b][q];
             }
             if (w < (uint32_t)(P.slot_bytes >> 2)) gw[w] = v;
         }
