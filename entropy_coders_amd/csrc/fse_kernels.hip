@@ -58,37 +58,96 @@ struct EncTab {
 // including the lane's first word, whose low bits belong to the previous
 // lane: the merge step later rewrites each boundary word with the OR of both
 // lanes' bits.
+// Bit writer of one lane's range: BitStackWriter order (writer.rs:140-222),
+// words through a 32-word LDS ring.  Every 16-word group of the slot that
+// lies wholly inside the lane's range leaves as one 64-byte store (four
+// dwordx4, a whole HBM burst) once the lane has moved past it; the partial
+// groups at either end leave as dword stores.  The lane's first word, when
+// it shares it with the lane above (off % 32 != 0), is never stored: its
+// value (head_val) goes to the merge list, like the lane's last partial
+// word.  Stores stay below wlim (the slot's words).
 struct Emit {
     uint64_t acc;
     uint32_t nacc;
-    uint32_t word;
+    uint32_t word;      // index of the word being filled
     uint32_t w0;        // first word index of the lane
-    uint32_t head_val;  // lane's bits of word w0 once it was stored
+    uint32_t head_val;  // lane's bits of word w0 (valid once word > w0 and the head group left)
     uint32_t wlim;      // words in the slot: stores never leave it
+    uint32_t gs;        // next 16-word group to store
+    bool skip_head;
     uint32_t* gw;
-    __device__ __forceinline__ void start(uint32_t* g, uint32_t off, uint32_t lim = 0xFFFFFFFFu) {
+    uint32_t* ring;     // LDS, 32 words, 16-byte aligned
+    __device__ __forceinline__ void start(uint32_t* g, uint32_t off, uint32_t lim = 0xFFFFFFFFu,
+                                          uint32_t* r = nullptr) {
         gw = g;
         wlim = lim;
+        ring = r;
         acc = 0;
         nacc = off & 31u;
         word = off >> 5;
         w0 = word;
+        gs = word >> 4;
+        skip_head = (off & 31u) != 0u;
         head_val = 0;
     }
     __device__ __forceinline__ void put(uint32_t v, uint32_t nb) {
         acc |= (uint64_t)v << nacc;
         nacc += nb;
     }
+    // The ring slot of the word being filled is written every time: until
+    // the word completes nothing reads it, so no branch is needed.
     __device__ __forceinline__ void flush() {
         const bool f = nacc >= 32u;
-        const uint32_t val = (uint32_t)acc;
-        if (f && word < wlim) gw[word] = val;
-        head_val = (f && word == w0) ? val : head_val;
+        ring[word & 31u] = (uint32_t)acc;
         acc = f ? (acc >> 32) : acc;
         nacc -= f ? 32u : 0u;
         word += f ? 1u : 0u;
     }
     __device__ __forceinline__ uint32_t pos() const { return word * 32u + nacc; }
+    __device__ __forceinline__ void store_words(uint32_t a, uint32_t b) {
+        for (uint32_t i = a; i < b; ++i)
+            if (i < wlim) gw[i] = ring[i & 31u];
+    }
+    __device__ __forceinline__ void store_group(uint32_t g) {
+        const uint32_t base = g << 4;
+        if (g == (w0 >> 4) && ((w0 & 15u) != 0u || skip_head)) {  // the lane's first group: its own words only
+            if (skip_head) head_val = ring[w0 & 31u];
+            store_words(skip_head ? w0 + 1u : w0, base + 16u);
+        } else if (base + 16u <= wlim) {
+            const uint4* r = reinterpret_cast<const uint4*>(ring + (base & 31u));
+            uint4* o = reinterpret_cast<uint4*>(gw + base);
+            const uint4 a = r[0], b = r[1], c = r[2], d = r[3];
+            o[0] = a;
+            o[1] = b;
+            o[2] = c;
+            o[3] = d;
+        }
+    }
+    // Store the group the lane has moved past, if any (called every <= 8
+    // pairs: <= 6 new words, so the ring never overruns a pending group).
+    __device__ __forceinline__ void drain() {
+        if (word >= (gs + 1u) << 4) {
+            store_group(gs);
+            ++gs;
+        }
+    }
+    // End of the lane: remaining whole groups, then the whole words of the
+    // last group (the partial word stays in acc for the merge list).
+    __device__ __forceinline__ void finish() {
+        while (word >= (gs + 1u) << 4) {
+            store_group(gs);
+            ++gs;
+        }
+        uint32_t lo = gs << 4;
+        if (gs == (w0 >> 4)) {
+            lo = w0;
+            if (skip_head) {
+                lo = w0 + 1u;
+                if (word > w0) head_val = ring[w0 & 31u];
+            }
+        }
+        store_words(lo, word);
+    }
 };
 
 struct Ckpt {
@@ -241,6 +300,7 @@ __device__ __forceinline__ EncState enc_range(const uint8_t* __restrict__ blk, u
     if (pb & ((1u << CS) - 1u)) {  // partial topmost chunk
         const uint4 q = load_chunk(blk, n, (uint32_t)c_hi);
         enc_chunk<MODE, false, NS>(q, (uint32_t)c_hi << CS, pb, x0, x1, T, bits, em);
+        if (MODE == PASS_EMIT) em.drain();
         if (MODE == PASS_EMIT && ck.base && (((uint32_t)c_hi << CS) & ck.mask) == 0u)
             ckpt_record<NS>(ck, (uint32_t)c_hi << CS, em.pos(), x0, x1);
         if (TRACK) track();
@@ -251,6 +311,7 @@ __device__ __forceinline__ EncState enc_range(const uint8_t* __restrict__ blk, u
     uint4 q0 = ld(c_hi), q1 = ld(c_hi - 1), q2 = ld(c_hi - 2), q3 = ld(c_hi - 3);
     auto body = [&](const uint4& q, int32_t c) {
         enc_chunk<MODE, true, NS>(q, (uint32_t)c << CS, pb, x0, x1, T, bits, em);
+        if (MODE == PASS_EMIT) em.drain();
         if (MODE == PASS_EMIT && ck.base && (((uint32_t)c << CS) & ck.mask) == 0u)
             ckpt_record<NS>(ck, (uint32_t)c << CS, em.pos(), x0, x1);
         if (TRACK) track();
@@ -338,7 +399,11 @@ struct EncSmem {
             uint32_t cnt[256];
         } p1;
         struct {
-            uint2 cp[64 * 8];  // count-pass trajectories (Track), 8 slots per lane
+            union {
+                uint2 cp[64 * 8];         // count-pass trajectories (Track), 8 slots per lane
+                uint32_t ring[64 * 36];   // emit: 32-word output ring per lane (stride 36: 16-byte
+                                          // aligned, conflict-free dwordx4 reads)
+            } u;
             uint32_t cntF[BPW][T + 1];
             uint32_t mword[BPW][2 * (T + 1)];
             uint32_t mval[BPW][2 * (T + 1)];
@@ -452,7 +517,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     // odd-length extra step), every other lane from a guessed start state,
     // recording its trajectory.  Then verify against the neighbour's end
     // state and repair by convergence (Track) until the fixed point.
-    Track tr{&sm.ph.p2.cp[lane * 8u], max(1u, (S / SPC + 7u) / 8u), false, 0u};
+    Track tr{&sm.ph.p2.u.cp[lane * 8u], max(1u, (S / SPC + 7u) / 8u), false, 0u};
     const uint32_t nslot = pb > pa ? (((pb - 1u) / SPC) - (pa / SPC)) / tr.ckc + 1u : 0u;
     uint32_t start = (1u << L) | (NS == 2 ? (1u << L) << 16 : 0u);
     uint32_t bits = 0;
@@ -513,7 +578,8 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     }
     __syncthreads();
     if (act && fits) {
-        em.start(gw, off, (P.debug & 4u) ? 0u : (uint32_t)(P.slot_bytes >> 2));  // debug bit 2: no payload stores (ablation)
+        em.start(gw, off, (P.debug & 4u) ? 0u : (uint32_t)(P.slot_bytes >> 2),  // debug bit 2: no payload stores (ablation)
+                 &sm.ph.p2.u.ring[lane * 36u]);
         if (P.sidecar && P.ckpt_interval) {
             ck.base = P.sidecar + gb * P.ckpt_per_block;
             ck.mask = P.ckpt_interval - 1u;
@@ -541,6 +607,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
             em.put(1u, 1u);
             em.flush();
         }
+        em.finish();
         // boundary words -> merge list (entry order = stream order)
         const uint32_t slot = 2u * (T - k);
         if ((off & 31u) != 0u && em.word > em.w0) {  // first word stored with the low bits empty
@@ -772,7 +839,7 @@ struct LdsChain {
         a1 = s1 << 2;
         B = 0;
         wlo = whi = wnx = 0;
-        if (VAR == 2) {
+        if (VAR == 2 || VAR == 6) {
             const int32_t k = max((p >> 5) - 1, 0);
             B = k << 5;
             wlo = pay[k];
@@ -793,6 +860,22 @@ struct LdsChain {
                 wlo = wnx;
                 wnx = pay[max((B >> 5) - 1, 0)];
             }
+        } else if (VAR == 6) {
+            // VAR 2's window with a branch-free refill: selects instead of an
+            // exec-masked branch, and the prefetch of the word below the
+            // window issued every pair (when no refill happened it re-reads
+            // the same word).  No SALU, no phi copies of in-flight loads.
+            e0 = *reinterpret_cast<const uint32_t*>(dtb + a0);
+            e1 = *reinterpret_cast<const uint32_t*>(dtb + a1);
+            pos -= (int32_t)((e0 + e1) & 0xFFu);
+            const uint32_t d = (uint32_t)(pos - B);  // in [8, 64]
+            x = (uint32_t)((((uint64_t)whi << 32) | wlo) >> d);
+            const bool c = d < 32u;
+            B = c ? B - 32 : B;
+            whi = c ? wlo : whi;
+            wlo = c ? wnx : wlo;
+            // word B/32 - 1 (B >= -32: the image has a 16-byte pad below it)
+            wnx = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(pay) + (B >> 3) - 4);
         } else if (VAR == 5) {
             // padded image + the window for this pair fetched together with
             // the table entries (its <= 24 bits lie in [pos - 24, pos))
@@ -1272,6 +1355,7 @@ __device__ __forceinline__ int32_t decode_segment1(RD& br, uint32_t s, uint32_t 
 
 template <int LMAX, uint32_t PMAX>
 struct PreSmem {
+    uint32_t pad[4];  // below the image: VAR 6 prefetches may address up to 2 words under it
     uint32_t pay[PMAX / 4];
     uint32_t dt[1u << LMAX];
     int err[16];
@@ -1388,7 +1472,12 @@ __global__ __launch_bounds__(64 * NW) void decode_pre_kernel(DecParams P) {
             if (r != FSE_OK) err = r;
         }
     } else
-    for (uint32_t seg = tid; seg < nseg; seg += NT) {
+    for (uint32_t base = 0; base < nseg; base += NT) {
+        // VAR 6: lane t decodes segment 33t mod NT of each round, so lanes
+        // that walk their segments in lockstep read words ~33 segments apart
+        // (spread over the banks) instead of ~1 segment (~32 words) apart
+        const uint32_t seg = base + (VAR == 6 ? ((tid * 33u) & (NT - 1u)) : tid);
+        if (seg >= nseg) continue;
         const uint64_t e = sc[seg];
         const uint32_t p0 = seg * I, p1 = min(p0 + I, Pm);
         const uint32_t bp = (uint32_t)e;
@@ -1666,6 +1755,7 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
             if (lmax <= 11) {
                 if (P.variant == 3) go(decode_pre_kernel<11, 8, PP, 3>, 512);
                 else if (P.variant == 5) go(decode_pre_kernel<11, 8, PP, 5>, 512);
+                else if (P.variant == 6) go(decode_pre_kernel<11, 8, PP, 6>, 512);
                 else go(decode_pre_kernel<11, 8, PP, 2>, 512);
             } else {
                 if (P.variant == 3) go(decode_pre_kernel<12, 8, PP - 8192, 3>, 512);
@@ -1680,6 +1770,7 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
                     else go(decode_pre_kernel<11, 4, PP, 2, 2, true>, 256);
                 } else if (P.variant == 3) go(decode_pre_kernel<11, 4, PP, 3>, 256);
                 else if (P.variant == 5) go(decode_pre_kernel<11, 4, PP, 5>, 256);
+                else if (P.variant == 6) go(decode_pre_kernel<11, 4, PP, 6>, 256);
                 else if (P.stage_kib == 40) go(decode_pre_kernel<11, 4, (40u << 10), 2>, 256);
                 else if (P.stage_kib == 36) go(decode_pre_kernel<11, 4, (36u << 10), 2>, 256);
                 else go(decode_pre_kernel<11, 4, PP, 2>, 256);
