@@ -67,7 +67,7 @@ struct EncTab {
 // value (head_val) goes to the merge list, like the lane's last partial
 // word.  Stores stay below wlim (the slot's words).
 struct Emit {
-    uint64_t acc;
+    uint32_t lo, hi;    // pending bits: lo = the word being filled, hi = bits past it
     uint32_t nacc;
     uint32_t word;      // index of the word being filled
     uint32_t w0;        // first word index of the lane
@@ -82,7 +82,7 @@ struct Emit {
         gw = g;
         wlim = lim;
         ring = r;
-        acc = 0;
+        lo = hi = 0;
         nacc = off & 31u;
         word = off >> 5;
         w0 = word;
@@ -91,16 +91,20 @@ struct Emit {
         head_val = 0;
     }
     __device__ __forceinline__ void put(uint32_t v, uint32_t nb) {
-        acc |= (uint64_t)v << nacc;
+        const uint64_t t = (uint64_t)v << nacc;  // nacc < 64
+        lo |= (uint32_t)t;
+        hi |= (uint32_t)(t >> 32);
         nacc += nb;
     }
     // The ring slot of the word being filled is written every time: until
-    // the word completes nothing reads it, so no branch is needed.
+    // the word completes nothing reads it, so no branch is needed.  Callers
+    // flush before nacc can reach 64 (<= 2 x 12 bits per flush).
     __device__ __forceinline__ void flush() {
         const bool f = nacc >= 32u;
-        ring[word & 31u] = (uint32_t)acc;
-        acc = f ? (acc >> 32) : acc;
-        nacc -= f ? 32u : 0u;
+        ring[word & 31u] = lo;
+        lo = f ? hi : lo;
+        hi = 0;  // nacc < 32 after the flush
+        nacc &= 31u;
         word += f ? 1u : 0u;
     }
     __device__ __forceinline__ uint32_t pos() const { return word * 32u + nacc; }
@@ -222,7 +226,7 @@ __device__ __forceinline__ void enc_chunk(const uint4& q, uint32_t c8, uint32_t 
             x0 = *reinterpret_cast<const uint16_t*>(T.st + ((x0 >> nb0) << 1) + (int32_t)t.y);
             if (MODE == PASS_COUNT || MODE == PASS_REPAIR) bits += nb0;
             if (MODE == PASS_EMIT) {
-                em.put(v0 & ((1u << nb0) - 1u), nb0);
+                em.put(__builtin_amdgcn_ubfe(v0, 0u, nb0), nb0);
                 if (j & 1) em.flush();  // <= 2 x 12 bits between flushes
             }
         }
@@ -239,7 +243,7 @@ __device__ __forceinline__ void enc_chunk(const uint4& q, uint32_t c8, uint32_t 
         x0 = *reinterpret_cast<const uint16_t*>(T.st + ((x0 >> nb0) << 1) + (int32_t)t0[j].y);
         if (MODE == PASS_COUNT || MODE == PASS_REPAIR) bits += nb1 + nb0;
         if (MODE == PASS_EMIT) {
-            const uint32_t pairbits = (v1 & ((1u << nb1) - 1u)) | ((v0 & ((1u << nb0) - 1u)) << nb1);
+            const uint32_t pairbits = (__builtin_amdgcn_ubfe(v0, 0u, nb0) << nb1) | __builtin_amdgcn_ubfe(v1, 0u, nb1);
             em.put(pairbits, nb1 + nb0);
             em.flush();
         }
@@ -616,7 +620,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
         }
         if (em.nacc) {  // last word never stored
             sm.ph.p2.mword[b][slot + 1] = em.word;
-            sm.ph.p2.mval[b][slot + 1] = (uint32_t)em.acc;
+            sm.ph.p2.mval[b][slot + 1] = em.lo;
         }
     }
     // header: whole words stored directly, the last partial word merged
