@@ -392,7 +392,7 @@ struct EncSmem {
     union {
         struct {
             union {
-                uint32_t hs[HIST_WORDS];  // sub-histograms; counts[] = hs[0..255] after the reduction
+                uint32_t hs[HIST_WORDS];  // sub-histograms (counts[] go to cnt[], free until the spread)
                 struct {
                     uint8_t sym_at[SIZE];
                     uint8_t occ_sym[SIZE];
@@ -436,13 +436,18 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
         const uint64_t off = gb * P.block_size;
         const uint32_t n = (uint32_t)min((uint64_t)P.block_size, P.n_total - off);
         const uint8_t* blk = P.src + off;
-        const uint32_t tl = wave_histogram(blk, n, sm.ph.p1.u.hs, sm.ph.p1.u.hs);
+        uint32_t* counts = sm.ph.p1.cnt;  // the spread reuses cnt[] after normalize
+        const uint32_t tl = wave_histogram(blk, n, sm.ph.p1.u.hs, counts);
         FSE_STAMP(P, 1);
+        if (P.debug & 8u) {  // ablation: histogram only
+            if (lane == 0) P.status[gb] = (int32_t)tl;
+            continue;
+        }
         int rc = FSE_OK;
         uint32_t Lreq = P.table_log, L = 0, slow = 0;
         if (n == 0) rc = FSE_ERR_EMPTY;
         if (rc == FSE_OK && P.table_log == 0) rc = optimal_log2(n, tl, &Lreq);  // histogram.rs:301
-        if (rc == FSE_OK) rc = wave_normalize(sm.ph.p1.u.hs, n, tl, Lreq, sm.ph.p1.norm, &L, &slow, sm.scratch);
+        if (rc == FSE_OK) rc = wave_normalize(counts, n, tl, Lreq, sm.ph.p1.norm, &L, &slow, sm.scratch);
         if (rc == FSE_OK && n < 2) rc = FSE_ERR_TOO_SHORT;  // lib.rs:154/156 unwrap
         if (rc == FSE_OK && L > (uint32_t)LMAX) rc = FSE_ERR_UNSUPPORTED;
         FSE_STAMP(P, 2);
@@ -494,7 +499,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     }
 
     FSE_STAMP(P, 4);
-    if (P.debug & 1u) return;  // ablation: statistics + tables only
+    if (P.debug & 9u) return;  // ablation: statistics + tables only (1), histogram only (8)
     // ---- phase 2: T lanes per block
     const int b = BPW == 1 ? 0 : (int)(lane / T);
     const uint32_t k = BPW == 1 ? lane : lane % T;

@@ -46,7 +46,7 @@ def main():
     ref = None
     for lanes in [int(x) for x in os.environ.get("ABL_LANES", "32,64").split(",")]:
         os.environ["FSEHIP_ENC_LANES"] = str(lanes)
-        for dbg, name in ((1, "tables_only"), (2, "no_emit"), (4, "no_payload_stores"), (0, "full")):
+        for dbg, name in ((8, "histogram_only"), (1, "tables_only"), (2, "no_emit"), (4, "no_payload_stores"), (0, "full")):
             os.environ["FSEHIP_DEBUG"] = str(dbg)
             res[f"enc_T{lanes}_{name}"] = timeit(lambda: codec.compress_into(src, cb))
         os.environ["FSEHIP_DEBUG"] = "0"

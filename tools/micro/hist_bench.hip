@@ -1,0 +1,111 @@
+// Histogram micro-benchmark (diagnostics, not part of the product): the
+// encoder's per-block 256-bin count (one 64-lane wave per 64 KiB block)
+// with different LDS sub-histogram layouts, on C2 data from fsehip_generate.
+// Build: hipcc -O3 --offload-arch=gfx950 hist_bench.hip -L../../entropy_coders_amd -lfsehip
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <vector>
+
+#include "../../include/fsehip.h"
+
+#define CK(x)                                                                        \
+    do {                                                                             \
+        hipError_t e = (x);                                                          \
+        if (e != hipSuccess) {                                                       \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); \
+            return 1;                                                                \
+        }                                                                            \
+    } while (0)
+
+constexpr uint32_t BS = 65536;
+
+// V: 0 = 4 x 257 u32 [sub][bin], sub = lane % 4 (current)
+//    1 = 8 x 256 u32 [bin][sub], sub = lane % 8
+//    2 = 16 x 256 u16 [bin][sub] packed in u32, sub = lane % 16
+//    3 = 8 x 257 u32 [sub][bin], sub = lane % 8
+//    4 = 16 x 257 u32 [sub][bin], sub = lane % 16
+template <int V>
+__global__ __launch_bounds__(64) void hist_kernel(const uint8_t* __restrict__ src, uint32_t* __restrict__ out) {
+    constexpr uint32_t WORDS = V == 0 ? 4 * 257 : V == 1 ? 8 * 256 : V == 2 ? 8 * 256 : V == 3 ? 8 * 257 : 16 * 257;
+    __shared__ uint32_t h[WORDS];
+    const uint32_t lane = threadIdx.x;
+    for (uint32_t i = lane; i < WORDS; i += 64) h[i] = 0;
+    __syncthreads();
+    const uint4* v4 = reinterpret_cast<const uint4*>(src + (uint64_t)blockIdx.x * BS);
+    auto add = [&](uint32_t b) {
+        if (V == 0) atomicAdd(&h[(lane & 3u) * 257u + b], 1u);
+        if (V == 1) atomicAdd(&h[b * 8u + (lane & 7u)], 1u);
+        if (V == 2) atomicAdd(&h[b * 8u + ((lane & 15u) >> 1)], 1u << (16u * (lane & 1u)));
+        if (V == 3) atomicAdd(&h[(lane & 7u) * 257u + b], 1u);
+        if (V == 4) atomicAdd(&h[(lane & 15u) * 257u + b], 1u);
+    };
+    constexpr uint32_t U = 8;
+    for (uint32_t v = 0; v < BS / 16; v += U * 64) {
+        uint4 d[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) d[u] = v4[v + u * 64 + lane];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint32_t w[4] = {d[u].x, d[u].y, d[u].z, d[u].w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) add((w[k] >> (8 * b)) & 0xFFu);
+        }
+    }
+    __syncthreads();
+    for (uint32_t s = lane; s < 256; s += 64) {
+        uint32_t c = 0;
+        if (V == 0) for (int q = 0; q < 4; ++q) c += h[q * 257 + s];
+        if (V == 1) for (int q = 0; q < 8; ++q) c += h[s * 8 + q];
+        if (V == 2) for (int q = 0; q < 8; ++q) { const uint32_t x = h[s * 8 + q]; c += (x & 0xFFFFu) + (x >> 16); }
+        if (V == 3) for (int q = 0; q < 8; ++q) c += h[q * 257 + s];
+        if (V == 4) for (int q = 0; q < 16; ++q) c += h[q * 257 + s];
+        out[(uint64_t)blockIdx.x * 256 + s] = c;
+    }
+}
+
+template <int V>
+int run(const uint8_t* d_src, uint32_t* d_out, uint32_t nb, std::vector<uint32_t>& ref, const char* name) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    hipLaunchKernelGGL(hist_kernel<V>, dim3(nb), dim3(64), 0, 0, d_src, d_out);
+    CK(hipDeviceSynchronize());
+    float best = 1e9f;
+    for (int r = 0; r < 5; ++r) {
+        CK(hipEventRecord(a));
+        hipLaunchKernelGGL(hist_kernel<V>, dim3(nb), dim3(64), 0, 0, d_src, d_out);
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b));
+        best = ms < best ? ms : best;
+    }
+    std::vector<uint32_t> h((size_t)nb * 256);
+    CK(hipMemcpy(h.data(), d_out, h.size() * 4, hipMemcpyDeviceToHost));
+    bool ok = true;
+    if (ref.empty()) ref = h; else ok = h == ref;
+    printf("%-32s %.4f ms  ok=%d\n", name, best, (int)ok);
+    return 0;
+}
+
+int main(int argc, char** argv) {
+    const int kind = argc > 1 ? atoi(argv[1]) : 0;
+    const double prob = argc > 2 ? atof(argv[2]) : 0.155;
+    const uint32_t nb = 16384;
+    uint8_t* d_src;
+    uint32_t* d_out;
+    CK(hipMalloc(&d_src, (size_t)nb * BS));
+    CK(hipMalloc(&d_out, (size_t)nb * 256 * 4));
+    if (fsehip_generate(kind, prob, 0x5EED0002ull, BS, d_src, (uint64_t)nb * BS, nullptr)) return 2;
+    CK(hipDeviceSynchronize());
+    std::vector<uint32_t> ref;
+    run<0>(d_src, d_out, nb, ref, "V0 4x257 [sub][bin] (current)");
+    run<1>(d_src, d_out, nb, ref, "V1 8 [bin][sub]");
+    run<2>(d_src, d_out, nb, ref, "V2 16 u16 [bin][sub]");
+    run<3>(d_src, d_out, nb, ref, "V3 8x257 [sub][bin]");
+    run<4>(d_src, d_out, nb, ref, "V4 16x257 [sub][bin]");
+    return 0;
+}
