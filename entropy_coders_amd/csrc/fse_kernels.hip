@@ -165,7 +165,7 @@ struct Ckpt {
 enum { PASS_SPEC = 0, PASS_COUNT = 1, PASS_EMIT = 2, PASS_REPAIR = 3 };
 
 // Trajectory of a count pass, for convergence-based repair: the state pair
-// and running bit count after every ckc-th chunk (at most 8 slots per lane,
+// and running bit count after every ckc-th chunk (at most TRACK_SLOTS slots per lane,
 // slot 0 = the lane's end).  A repair re-encodes from the corrected start
 // state only until it meets the recorded trajectory: from there on states
 // and bits are identical, so the lane's total follows from the record and
@@ -174,6 +174,9 @@ enum { PASS_SPEC = 0, PASS_COUNT = 1, PASS_EMIT = 2, PASS_REPAIR = 3 };
 // writes its running count there, and track_fixup turns the slots it wrote
 // into remaining counts once the pass total is known, so every slot stays
 // consistent with the lane's current trajectory.
+// Trajectory slots per lane.  16 (repairs stop sooner) measured slower
+// than 8 on C2: the count pass writes twice as many slots.
+constexpr uint32_t TRACK_SLOTS = 8;
 struct Track {
     uint2* cp;        // this lane's slots (LDS)
     uint32_t ckc;     // chunks per slot
@@ -404,7 +407,7 @@ struct EncSmem {
         } p1;
         struct {
             union {
-                uint2 cp[64 * 8];         // count-pass trajectories (Track), 8 slots per lane
+                uint2 cp[64 * TRACK_SLOTS];  // count-pass trajectories (Track)
                 uint32_t ring[64 * 36];   // emit: 32-word output ring per lane (stride 36: 16-byte
                                           // aligned, conflict-free dwordx4 reads)
             } u;
@@ -526,7 +529,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     // odd-length extra step), every other lane from a guessed start state,
     // recording its trajectory.  Then verify against the neighbour's end
     // state and repair by convergence (Track) until the fixed point.
-    Track tr{&sm.ph.p2.u.cp[lane * 8u], max(1u, (S / SPC + 7u) / 8u), false, 0u};
+    Track tr{&sm.ph.p2.u.cp[lane * TRACK_SLOTS], max(1u, (S / SPC + TRACK_SLOTS - 1u) / TRACK_SLOTS), false, 0u};
     const uint32_t nslot = pb > pa ? (((pb - 1u) / SPC) - (pa / SPC)) / tr.ckc + 1u : 0u;
     uint32_t start = (1u << L) | (NS == 2 ? (1u << L) << 16 : 0u);
     uint32_t bits = 0;
