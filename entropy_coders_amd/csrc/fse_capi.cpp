@@ -367,7 +367,9 @@ int fsehip_decompress_blocks_dt(const fsehip_params* p, const uint8_t* d_in, uin
                                 fsehip_stream_t stream) {
     if (n_total == 0) return FSE_ERR_EMPTY;
     if (!p || !d_dtables || !d_dtinfo) return FSE_ERR_BAD_ARG;
-    if ((!d_sidecar || p->ckpt_interval == 0) && p->nstates != 1) return FSE_ERR_BAD_ARG;  // 1-state: serial without one
+    if (d_sidecar && p->ckpt_interval == 0) return FSE_ERR_BAD_ARG;
+    // without a sidecar: 2-state blocks take the speculative sync decoder,
+    // 1-state blocks the serial one
     fsehip_params q = *p;
     q.max_table_log = dt_lmax(p);  // the table stride the tables were built with
     return decompress_impl(&q, d_in, slot_bytes, d_comp_len, d_sidecar, d_out, n_total, nullptr, d_status, nullptr,
@@ -380,7 +382,8 @@ int fsehip_decompress_blocks(const fsehip_params* p, const uint8_t* d_in, uint64
                              int32_t* d_status, fsehip_stream_t stream) {
     if (n_total == 0) return FSE_ERR_EMPTY;
     if (d_sidecar && p && p->ckpt_interval == 0) return FSE_ERR_BAD_ARG;
-    if (p && (p->nstates == 1 || (d_sidecar && !env_u32("FSEHIP_DEC_FUSED", 0)))) {
+    // FSEHIP_DEC_FUSED=1: the one-kernel path (serial one lane per block without a sidecar)
+    if (p && (p->nstates == 1 || !env_u32("FSEHIP_DEC_FUSED", 0))) {
         // two kernels: decode tables for all blocks at high occupancy, then
         // the LDS-heavy segment decode with no serial phase
         const uint32_t bs = p->block_size ? p->block_size : kDefaultBlock;
@@ -402,6 +405,22 @@ int fsehip_build_sidecar(const fsehip_params* p, const uint8_t* d_in, uint64_t s
                          const uint32_t* d_comp_len, uint8_t* d_out, uint64_t n_total, uint64_t* d_sidecar_out,
                          int32_t* d_status, fsehip_stream_t stream) {
     if (n_total == 0) return FSE_ERR_EMPTY;
+    if (p && p->nstates != 1 && d_sidecar_out && !env_u32("FSEHIP_DEC_FUSED", 0)) {
+        // tables for all blocks, then the serial decoder (table in LDS, 20 blocks per CU) records it
+        if (p->ckpt_interval < 8 || (p->ckpt_interval & (p->ckpt_interval - 1))) return FSE_ERR_BAD_ARG;
+        const uint32_t bs = p->block_size ? p->block_size : kDefaultBlock;
+        const uint64_t n_blocks = (n_total + bs - 1) / bs;
+        if (!device_ok()) return FSE_ERR_NO_DEVICE;
+        uint32_t* dt = static_cast<uint32_t*>(scratch(stream, SCRATCH_DT, fsehip_dtable_bytes(p->max_table_log) * n_blocks));
+        int32_t* info = static_cast<int32_t*>(scratch(stream, SCRATCH_DTINFO, 4ull * n_blocks));
+        if (!dt || !info) return FSE_ERR_HIP;
+        int rc = fsehip_build_dtables(p, d_in, slot_bytes, d_comp_len, (uint32_t)n_blocks, dt, info, stream);
+        if (rc != FSE_OK) return rc;
+        fsehip_params q = *p;
+        q.max_table_log = dt_lmax(p);
+        return decompress_impl(&q, d_in, slot_bytes, d_comp_len, nullptr, d_out, n_total, d_sidecar_out, d_status,
+                               nullptr, 0, stream, dt, info);
+    }
     return decompress_impl(p, d_in, slot_bytes, d_comp_len, nullptr, d_out, n_total, d_sidecar_out, d_status,
                            nullptr, 0, stream);
 }

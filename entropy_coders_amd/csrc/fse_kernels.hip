@@ -1624,6 +1624,168 @@ __global__ __launch_bounds__(64) void decode1_serial_kernel(DecParams P) {
 }
 
 // ------------------------------------------------------------------------
+// Sidecar-less container decode of 2-state blocks (any valid fse_compress2
+// stream, e.g. from the CPU crate), optionally recording the sidecar.
+// The two interleaved decoders make the stream essentially serial: a
+// decoder started mid-block with guessed states practically never falls
+// into step with the exact one (tools/syncsim.py: 35 of 40 random starts in
+// a C2 block never did, the rest after 25K-40K symbols), so speculative
+// segment decoding cannot replace the sidecar for this
+// format.  The serial decode is instead made as short a dependency chain
+// as possible and run at high occupancy: the block's prebuilt table sits in
+// LDS (8 KiB -> 20 blocks in flight per CU), one lane walks the stream
+// (lib.rs:227-244, container mode as the oracle's decompress2 with known
+// length) and the bits come through a register window fed from 16-byte
+// chunks that are loaded a whole chunk ahead.
+// ------------------------------------------------------------------------
+struct ChunkReader {
+    const uint4* w4;  // the block as 16-byte quads
+    uint64_t buf;     // stream bits [base, base + 64)
+    int32_t base, pos;
+    uint4 cl, ch, nl, nh;  // chunk c (words 8c..8c+7) and chunk c-1, loading
+    int32_t c;
+    __device__ __forceinline__ void init(const uint8_t* in, int32_t p) {
+        w4 = reinterpret_cast<const uint4*>(in);
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(in);
+        pos = p;
+        base = max(((p + 31) & ~31) - 64, 0);
+        buf = (uint64_t)w[base >> 5] | ((uint64_t)w[(base >> 5) + 1] << 32);
+        c = ((base >> 5) - 1) >> 3;  // chunk of the next word to enter the window
+        cl = w4[2 * max(c, 0)];
+        ch = w4[2 * max(c, 0) + 1];
+        nl = w4[2 * max(c - 1, 0)];
+        nh = w4[2 * max(c - 1, 0) + 1];
+    }
+    __device__ __forceinline__ uint32_t pop(uint32_t nb) {
+        pos -= (int32_t)nb;
+        return (uint32_t)(buf >> (uint32_t)(pos - base)) & ((1u << nb) - 1u);
+    }
+    __device__ __forceinline__ void refill() {
+        if (pos - base < 32 && base > 0) {
+            base -= 32;
+            const int32_t wi = base >> 5;
+            if ((wi >> 3) != c) {  // every 8th refill: move down a chunk, prefetch the next
+                cl = nl;
+                ch = nh;
+                c -= 1;
+                nl = w4[2 * max(c - 1, 0)];
+                nh = w4[2 * max(c - 1, 0) + 1];
+            }
+            const uint32_t j = (uint32_t)wi & 7u;
+            const uint4 q = j < 4u ? cl : ch;
+            const uint32_t k = j & 3u;
+            const uint32_t v = k == 0 ? q.x : k == 1 ? q.y : k == 2 ? q.z : q.w;
+            buf = (buf << 32) | v;
+        }
+    }
+};
+
+// One lane per block; the rest of the wave only stages the table.  (An LDS
+// ring for the stream and the output, flushed by the whole wave every 128
+// pairs, measured slower: its 10.7 KB per block allow 14 blocks per CU
+// instead of 20, and the chain is latency-bound either way.)
+template <int LMAX>
+__global__ __launch_bounds__(64) void serial2_decode_kernel(DecParams P) {
+    __shared__ uint32_t tab[1u << LMAX];
+    const uint64_t gb = blockIdx.x;
+    if (gb >= P.n_blocks) return;
+    const int32_t info = P.dtinfo[gb];
+    const uint32_t lane = threadIdx.x;
+    if (info >= 0) {  // stage the table (prebuilt by dtable_blocks_kernel)
+        const uint32_t nv = (1u << ((uint32_t)info >> 16)) >> 2;  // 16-byte chunks
+        const uint4* t4 = reinterpret_cast<const uint4*>(P.dt + gb * (uint64_t)(1u << LMAX));
+        uint4* d4 = reinterpret_cast<uint4*>(tab);
+        for (uint32_t i = lane; i < nv; i += 64u) d4[i] = t4[i];
+    }
+    __syncthreads();
+    if (lane != 0) return;
+    const uint8_t* in = P.in + gb * P.slot_bytes;
+    const uint32_t clen = P.comp_len[gb];
+    const uint64_t ooff = gb * (uint64_t)P.block_size;
+    const uint32_t n = (uint32_t)min((uint64_t)P.block_size, P.n_total - ooff);
+    uint8_t* out = P.out + ooff;
+    int32_t err = info < 0 ? info : (n < 2 ? FSE_ERR_LENGTH_MISMATCH : FSE_OK);
+    const int32_t hdr_bits = (info & 0xFFFF) * 8;
+    const uint32_t L = (uint32_t)info >> 16;
+    uint32_t o = 0;
+    if (err == FSE_OK) {
+        const int32_t top = (int32_t)(clen - 1u) * 8 + (int32_t)ilog2u(in[clen - 1]);
+        if (top - 2 * (int32_t)L < hdr_bits) err = FSE_ERR_TOO_SHORT;  // lib.rs:224-225
+    }
+    if (err == FSE_OK) {
+        ChunkReader br;
+        br.init(in, (int32_t)(clen - 1u) * 8 + (int32_t)ilog2u(in[clen - 1]));
+        uint32_t s0 = br.pop(L);
+        br.refill();
+        uint32_t s1 = br.pop(L);
+        br.refill();
+        const uint32_t I = P.ckpt_interval;
+        uint64_t* rec = (P.sidecar_out && I) ? P.sidecar_out + gb * P.ckpt_per_block : nullptr;
+        const uint32_t ckmask = I ? I - 1u : 0u;
+        uint32_t pidx = 0;
+        auto record = [&]() {
+            if (rec && (pidx & ckmask) == 0u && pidx / I < P.ckpt_per_block)
+                rec[pidx / I] = (uint64_t)(uint32_t)(br.pos - hdr_bits) | ((uint64_t)s0 << 32) | ((uint64_t)s1 << 48);
+        };
+        // bulk: groups of 8 pairs that can neither reach the raw length nor
+        // run out of bits (<= 2 x 12 bits a pair): no end checks, and the
+        // 16 output bytes leave as one dwordx4 store, so few stores are in
+        // flight when the next chunk's load is waited on
+        while (o + 18u < n && br.pos - hdr_bits >= 8 * 24) {
+            uint32_t w[4];
+#pragma unroll
+            for (uint32_t j = 0; j < 8u; ++j, ++pidx) {
+                record();
+                const uint32_t e0 = tab[s0];
+                s0 = dte_ns(e0) + br.pop(dte_nb(e0));
+                br.refill();
+                const uint32_t e1 = tab[s1];
+                s1 = dte_ns(e1) + br.pop(dte_nb(e1));
+                br.refill();
+                const uint32_t v = dte_sym(e0) | (dte_sym(e1) << 8);
+                if (j & 1u) w[j >> 1] |= v << 16; else w[j >> 1] = v;
+            }
+            if (!(P.debug & 2u)) *reinterpret_cast<uint4*>(out + o) = make_uint4(w[0], w[1], w[2], w[3]);  // 2: ablation
+            o += 16;
+        }
+        // tail: pair by pair with the reference's end checks
+        for (;; ++pidx) {
+            record();
+            if (o + 2u >= n) {  // the raw length ends the block (o is even here)
+                if (o < n) out[o++] = (uint8_t)dte_sym(tab[s0]);
+                if (o < n) out[o++] = (uint8_t)dte_sym(tab[s1]);
+                break;
+            }
+            const uint32_t e0 = tab[s0];
+            uint32_t nb = dte_nb(e0);
+            if (br.pos - (int32_t)nb < hdr_bits) {  // decoder 0 cannot read: lib.rs:242-243
+                out[o++] = (uint8_t)dte_sym(e0);
+                out[o++] = (uint8_t)dte_sym(tab[s1]);
+                break;
+            }
+            s0 = dte_ns(e0) + br.pop(nb);
+            br.refill();
+            const uint32_t e1 = tab[s1];
+            nb = dte_nb(e1);
+            if (br.pos - (int32_t)nb < hdr_bits) {  // decoder 1 cannot read: lib.rs:235-239
+                out[o++] = (uint8_t)dte_sym(e0);
+                out[o++] = (uint8_t)dte_sym(e1);
+                if (o < n) out[o++] = (uint8_t)dte_sym(tab[s0]);
+                break;
+            }
+            s1 = dte_ns(e1) + br.pop(nb);
+            br.refill();
+            out[o] = (uint8_t)dte_sym(e0);
+            out[o + 1] = (uint8_t)dte_sym(e1);
+            o += 2;
+        }
+        if (o != n) err = FSE_ERR_LENGTH_MISMATCH;
+    }
+    P.status[gb] = err;
+    if (P.out_len) P.out_len[gb] = err ? 0u : o;
+}
+
+// ------------------------------------------------------------------------
 // Histogram::new per block (histogram::count), one wave per block.
 // ------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void histogram_blocks_kernel(const uint8_t* src, uint64_t n_total,
@@ -1749,6 +1911,11 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
     // LDS stage for the compressed block, sized for 3 workgroups per CU at L <= 11
     constexpr uint32_t PM4 = 39u << 10, PM8 = 35u << 10;
     const dim3 g(P.n_blocks);
+    if (P.dt && !P.sidecar && P.nstates != 1 && P.n_total) {  // sidecar-less container blocks
+        if (lmax <= 11) hipLaunchKernelGGL((serial2_decode_kernel<11>), g, dim3(64), 0, stream, P);
+        else hipLaunchKernelGGL((serial2_decode_kernel<12>), g, dim3(64), 0, stream, P);
+        return hipGetLastError();
+    }
     if (P.dt) {  // prebuilt tables: lean kernel; LDS = image + table (44 KB image -> 3 WG/CU)
         constexpr uint32_t PP = 44u << 10;
         auto go = [&](auto kern, uint32_t threads) { hipLaunchKernelGGL(kern, g, dim3(threads), 0, stream, P); };

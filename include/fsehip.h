@@ -97,8 +97,9 @@ int fsehip_compress_blocks(const fsehip_params* p, const uint8_t* d_src, uint64_
                            uint64_t* d_sidecar, int32_t* d_status, fsehip_stream_t stream);
 
 /* Decompress blocks produced as above.  With d_sidecar the blocks decode in
- * parallel segments; without it each block decodes serially (any valid
- * fse_compress2 stream).  n_total (> 0) gives the raw length. */
+ * parallel segments; without it (any valid fse_compress2 stream, e.g. from
+ * the CPU crate) each block decodes serially, at high occupancy (its table
+ * in LDS, 20 blocks in flight per CU).  n_total (> 0) gives the raw length. */
 int fsehip_decompress_blocks(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
                              const uint32_t* d_comp_len, const uint64_t* d_sidecar, uint8_t* d_out,
                              uint64_t n_total, int32_t* d_status, fsehip_stream_t stream);
@@ -112,8 +113,9 @@ uint64_t fsehip_dtable_bytes(uint32_t max_table_log);
 int fsehip_build_dtables(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
                          const uint32_t* d_comp_len, uint32_t n_blocks, uint32_t* d_dtables, int32_t* d_dtinfo,
                          fsehip_stream_t stream);
-/* Decompress with prebuilt tables (requires the sidecar).  fsehip_decompress_blocks
- * with a sidecar runs fsehip_build_dtables + this into a per-stream workspace. */
+/* Decompress with prebuilt tables, with or without the sidecar (as above).
+ * fsehip_decompress_blocks runs fsehip_build_dtables + this into a
+ * per-stream workspace. */
 int fsehip_decompress_blocks_dt(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
                                 const uint32_t* d_comp_len, const uint64_t* d_sidecar, const uint32_t* d_dtables,
                                 const int32_t* d_dtinfo, uint8_t* d_out, uint64_t n_total, int32_t* d_status,
