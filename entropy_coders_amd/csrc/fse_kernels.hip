@@ -924,10 +924,11 @@ struct LdsChain {
 
 // 32 pairs = one whole 64-byte segment of output per lane, stored back to
 // back (full HBM write bursts instead of masked partial ones).
+template <uint32_t GRP = DEC_GROUP>
 __device__ __forceinline__ void store_group(uint8_t* __restrict__ dst, const uint32_t* w) {
     uint4* o4 = reinterpret_cast<uint4*>(dst);
 #pragma unroll
-    for (uint32_t q = 0; q < DEC_GROUP / 8u; ++q) o4[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+    for (uint32_t q = 0; q < GRP / 8u; ++q) o4[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
 }
 
 // Pairs [p, p1) of one chain, then (when `last`) the reference termination
@@ -997,11 +998,14 @@ __device__ __forceinline__ int32_t decode_dual(const uint32_t* pay, const uint8_
                                                uint32_t pa1, bool lastA, LdsChain<VAR>& Bc, uint32_t pb, uint32_t pb1,
                                                bool lastB, uint32_t n, uint32_t Pm, uint8_t* __restrict__ out,
                                                int32_t hdr_bits) {
-    const uint32_t common = min(pa1 - pa, pb1 - pb) / DEC_GROUP * DEC_GROUP;
-    for (uint32_t k = 0; k < common; k += DEC_GROUP) {
-        uint32_t wa[DEC_GROUP / 2u], wb[DEC_GROUP / 2u];
+    // 16 pairs (32 B) per chain between stores: two chains' output buffers
+    // in registers at once
+    constexpr uint32_t GRP = 16u;
+    const uint32_t common = min(pa1 - pa, pb1 - pb) / GRP * GRP;
+    for (uint32_t k = 0; k < common; k += GRP) {
+        uint32_t wa[GRP / 2u], wb[GRP / 2u];
 #pragma unroll
-        for (uint32_t j = 0; j < DEC_GROUP; j += 2u) {
+        for (uint32_t j = 0; j < GRP; j += 2u) {
             const uint32_t la = A.pair(pay, dtb);
             const uint32_t lb = Bc.pair(pay, dtb);
             const uint32_t ha = A.pair(pay, dtb);
@@ -1009,8 +1013,8 @@ __device__ __forceinline__ int32_t decode_dual(const uint32_t* pay, const uint8_
             wa[j >> 1] = __builtin_amdgcn_perm(ha, la, 0x05040100u);
             wb[j >> 1] = __builtin_amdgcn_perm(hb, lb, 0x05040100u);
         }
-        store_group(out + 2u * (pa + k), wa);
-        store_group(out + 2u * (pb + k), wb);
+        store_group<GRP>(out + 2u * (pa + k), wa);
+        store_group<GRP>(out + 2u * (pb + k), wb);
     }
     const int32_t ra = run_chain(A, pay, dtb, pa + common, pa1, lastA, n, Pm, out, hdr_bits);
     const int32_t rb = run_chain(Bc, pay, dtb, pb + common, pb1, lastB, n, Pm, out, hdr_bits);
