@@ -119,13 +119,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU over RCCL ("nccl"); FSEHIP_BENCH_BACKEND=gloo rehearses the
+    # multi-rank logic on a one-GPU box (ranks share the card, CPU collectives)
+    backend = os.environ.get("FSEHIP_BENCH_BACKEND", "nccl")
+    gpu = local % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    cdev = dev if backend == "nccl" else torch.device("cpu")  # where collective tensors live
 
     from entropy_coders_amd import BlockCodec
 
@@ -141,7 +147,10 @@ def main():
 
     def barrier():
         if world > 1:
-            dist.barrier(device_ids=[local])
+            if backend == "nccl":
+                dist.barrier(device_ids=[gpu])
+            else:
+                dist.barrier()
 
     for _ in range(args.warmup):
         codec.compress_into(src, cb)
@@ -163,7 +172,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -180,7 +189,7 @@ def main():
 
     side_bytes = 8 * sum(n_ckpt(min(args.block, n - b * args.block)) for b in range(nb)) if args.ckpt else 0
     if world > 1:
-        flag = torch.tensor([1 if ok else 0], device=dev)
+        flag = torch.tensor([1 if ok else 0], device=cdev)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         ok = bool(flag.item())
 
