@@ -167,6 +167,22 @@ class BlockCodec:
         self.decompress_into(cb, out, status, use_sidecar)
         return out, status
 
+    def build_sidecar(self, cb: dict):
+        """`fsehip_build_sidecar`: decode blocks that carry no sidecar (e.g.
+        from the CPU crate) and record their sidecar.  Returns (out, sidecar,
+        status) device tensors."""
+        t = self.torch
+        nb = self.n_blocks(cb["n_total"])
+        out = t.empty(cb["n_total"], dtype=t.uint8, device=self.device)
+        side = t.zeros(max(nb * self.side_per_block, 1), dtype=t.int64, device=self.device)
+        status = t.zeros(nb, dtype=t.int32, device=self.device)
+        p = self.params()
+        check(self.lib.fsehip_build_sidecar(
+            C.byref(p), C.c_void_p(cb["out"].data_ptr()), self.slot_bytes, C.c_void_p(cb["comp_len"].data_ptr()),
+            C.c_void_p(out.data_ptr()), cb["n_total"], C.c_void_p(side.data_ptr()), C.c_void_p(status.data_ptr()),
+            self._stream()), "fsehip_build_sidecar")
+        return out, side, status
+
     def build_dtables(self, cb: dict) -> dict:
         """Decode tables for every block of `cb` (fsehip_build_dtables): the
         pre-built tables of decode-only workloads (C3)."""

@@ -56,3 +56,36 @@ def test_host_pipeline_roundtrip(torch_cuda, nstates, ckpt, chunk):
     out, dstat = pipe.decompress(stream, lens, side, n)
     assert int(dstat.abs().max()) == 0
     assert torch.equal(out, host)
+
+
+@pytest.mark.parametrize("ckpt", [64, 128, 512])
+def test_build_sidecar_matches_encoder(torch_cuda, ckpt):
+    """Blocks compressed without a sidecar (as from the CPU crate): the
+    serial decoder restores them and records the same sidecar the encoder
+    would have written; the parallel decoder then uses it."""
+    torch = torch_cuda
+    from entropy_coders_amd import BlockCodec
+
+    n = 9 * 65536 + 1001
+    ref = BlockCodec(ckpt_interval=ckpt)
+    src = ref.generate(1, 0.5, 0x5EED0F05, n)
+    cb_ref = ref.compress(src)
+    bare = BlockCodec(ckpt_interval=0)
+    cb = bare.compress(src)  # no sidecar
+    torch.cuda.synchronize()
+    out, side, st = ref.build_sidecar(cb)
+    torch.cuda.synchronize()
+    assert int(st.abs().max()) == 0
+    assert torch.equal(out, src)
+    spb = ref.side_per_block
+    want = cb_ref["sidecar"].cpu()
+    got = side.cpu()
+    for b in range(ref.n_blocks(n)):
+        nb_ = min(65536, n - b * 65536)
+        pm = (nb_ - 3) // 2 if nb_ & 1 else nb_ // 2 - 1
+        k = pm // ckpt + 1
+        assert torch.equal(got[b * spb: b * spb + k], want[b * spb: b * spb + k]), f"block {b}"
+    cb["sidecar"] = side
+    out2, st2 = ref.decompress(cb)
+    torch.cuda.synchronize()
+    assert int(st2.abs().max()) == 0 and torch.equal(out2, src)
