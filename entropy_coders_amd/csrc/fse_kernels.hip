@@ -1684,10 +1684,12 @@ struct ChunkReader {
     }
 };
 
-// One lane per block; the rest of the wave only stages the table.  (An LDS
-// ring for the stream and the output, flushed by the whole wave every 128
-// pairs, measured slower: its 10.7 KB per block allow 14 blocks per CU
-// instead of 20, and the chain is latency-bound either way.)
+// One lane per block; the rest of the wave only stages the table.  Measured
+// slower and dropped: an LDS ring for the stream and the output, flushed by
+// the whole wave every 128 pairs (its 10.7 KB per block allow 14 blocks per
+// CU instead of 20, and the chain is latency-bound either way), and a
+// scalar-unit walk with all state in SGPRs (26.5 vs 15.9 ms per 256 MiB:
+// the CU's one scalar unit is shared by the 20 blocks in flight).
 template <int LMAX>
 __global__ __launch_bounds__(64) void serial2_decode_kernel(DecParams P) {
     __shared__ uint32_t tab[1u << LMAX];
