@@ -133,3 +133,53 @@ def test_pack_unpack(torch_cuda):
     out, st = codec.decompress(cb2)
     torch.cuda.synchronize()
     assert int(st.abs().max()) == 0 and torch.equal(out, src)
+
+
+@pytest.mark.parametrize("use_sidecar", [True, False])
+def test_corrupt_blocks_fail_cleanly(torch_cuda, use_sidecar):
+    """Damaged blocks (flipped payload bytes, broken headers, truncated
+    lengths, a bad sidecar entry) must come back as per-block statuses or
+    garbage bytes -- never a fault, a hang or a write outside the block."""
+    torch = torch_cuda
+    from entropy_coders_amd import BlockCodec
+
+    block = 65536
+    nb = 12
+    codec = BlockCodec(block_size=block, ckpt_interval=128)
+    src = codec.generate(0, 0.155, 0x5EED0F06, nb * block)
+    cb = codec.compress(src)
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(7)
+    slots = cb["out"].cpu().numpy().copy()
+    lens = cb["comp_len"].cpu().numpy().copy()
+    side = cb["sidecar"].cpu().numpy().copy()
+    sb = codec.slot_bytes
+    for b in range(nb):
+        base, ln = b * sb, int(lens[b])
+        kind = b % 6
+        if kind == 1:  # flipped payload bytes
+            for i in rng.integers(64, ln - 1, 20):
+                slots[base + i] ^= 0xA5
+        elif kind == 2:  # broken header bytes
+            slots[base: base + 8] = rng.integers(0, 256, 8, dtype=np.uint8)
+        elif kind == 3:  # truncated (last byte may become 0: no marker)
+            lens[b] = ln // 2
+        elif kind == 4:  # marker byte cleared
+            slots[base + ln - 1] = 0
+        elif kind == 5:  # a sidecar entry pointing past the block
+            side[b * codec.side_per_block + 3] = np.int64(0x7FFFFFF0)
+    cb["out"] = torch.from_numpy(slots).to(codec.device)
+    cb["comp_len"] = torch.from_numpy(lens).to(codec.device)
+    cb["sidecar"] = torch.from_numpy(side).to(codec.device)
+    # a guard region after the output catches writes past the last block
+    buf = torch.full((nb * block + 4096,), 0x5A, dtype=torch.uint8, device=codec.device)
+    st = torch.zeros(nb, dtype=torch.int32, device=codec.device)
+    codec.decompress_into(cb, buf[: nb * block], st, use_sidecar=use_sidecar)
+    torch.cuda.synchronize()
+    status = st.cpu().numpy()
+    assert bool((buf[nb * block:] == 0x5A).all()), "write past the output"
+    for b in range(nb):
+        if b % 6 == 0:
+            assert status[b] == 0 and torch.equal(buf[b * block:(b + 1) * block], src[b * block:(b + 1) * block])
+    for b in (3, 4, 9, 10):  # truncated / marker cleared: always detected
+        assert status[b] != 0, (b, status)
