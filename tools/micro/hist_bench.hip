@@ -66,17 +66,67 @@ __global__ __launch_bounds__(64) void hist_kernel(const uint8_t* __restrict__ sr
     }
 }
 
+// V5: per-lane private 8-bit counters, [bin/4][lane] dwords (conflict-free
+// atomics: each lane owns its dwords), flushed into u32 totals every 128
+// bytes per lane (a counter gains <= 128 per round).
+__global__ __launch_bounds__(64) void hist_kernel_v5(const uint8_t* __restrict__ src, uint32_t* __restrict__ out) {
+    __shared__ uint32_t c8[64 * 64];   // 64 dwords (256 bins) per lane, [q][lane]
+    __shared__ uint32_t tot[256];
+    const uint32_t lane = threadIdx.x;
+    for (uint32_t i = lane; i < 64 * 64; i += 64) c8[i] = 0;
+    for (uint32_t i = lane; i < 256; i += 64) tot[i] = 0;
+    __syncthreads();
+    const uint4* v4 = reinterpret_cast<const uint4*>(src + (uint64_t)blockIdx.x * BS);
+    uint32_t acc_lo = 0, acc_hi = 0;  // this lane's bins 4*lane .. 4*lane+3 (pairs of u16)
+    constexpr uint32_t U = 8;
+    for (uint32_t v = 0; v < BS / 16; v += U * 64) {
+        uint4 d[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) d[u] = v4[v + u * 64 + lane];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint32_t w[4] = {d[u].x, d[u].y, d[u].z, d[u].w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const uint32_t sym = (w[k] >> (8 * b)) & 0xFFu;
+                    atomicAdd(&c8[(sym >> 2) * 64 + lane], 1u << (8u * (sym & 3u)));
+                }
+        }
+        __syncthreads();
+        // flush: lane l sums dword q = l over all lanes (rotated reads: conflict-free), then clears
+        for (uint32_t j = 0; j < 64; ++j) {
+            const uint32_t src_lane = (j + lane) & 63u;
+            const uint32_t x = c8[lane * 64 + src_lane];
+            acc_lo += x & 0x00FF00FFu;
+            acc_hi += (x >> 8) & 0x00FF00FFu;
+        }
+        __syncthreads();
+        for (uint32_t j = 0; j < 64; ++j) c8[lane * 64 + ((j + lane) & 63u)] = 0;
+        __syncthreads();
+    }
+    out[(uint64_t)blockIdx.x * 256 + 4 * lane + 0] = acc_lo & 0xFFFFu;
+    out[(uint64_t)blockIdx.x * 256 + 4 * lane + 1] = acc_hi & 0xFFFFu;
+    out[(uint64_t)blockIdx.x * 256 + 4 * lane + 2] = acc_lo >> 16;
+    out[(uint64_t)blockIdx.x * 256 + 4 * lane + 3] = acc_hi >> 16;
+}
+
 template <int V>
 int run(const uint8_t* d_src, uint32_t* d_out, uint32_t nb, std::vector<uint32_t>& ref, const char* name) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
-    hipLaunchKernelGGL(hist_kernel<V>, dim3(nb), dim3(64), 0, 0, d_src, d_out);
+    auto launch = [&]() {
+        if (V == 5) hipLaunchKernelGGL(hist_kernel_v5, dim3(nb), dim3(64), 0, 0, d_src, d_out);
+        else hipLaunchKernelGGL(hist_kernel<V == 5 ? 0 : V>, dim3(nb), dim3(64), 0, 0, d_src, d_out);
+    };
+    launch();
     CK(hipDeviceSynchronize());
     float best = 1e9f;
     for (int r = 0; r < 5; ++r) {
         CK(hipEventRecord(a));
-        hipLaunchKernelGGL(hist_kernel<V>, dim3(nb), dim3(64), 0, 0, d_src, d_out);
+        launch();
         CK(hipEventRecord(b));
         CK(hipEventSynchronize(b));
         float ms;
@@ -107,5 +157,6 @@ int main(int argc, char** argv) {
     run<2>(d_src, d_out, nb, ref, "V2 16 u16 [bin][sub]");
     run<3>(d_src, d_out, nb, ref, "V3 8x257 [sub][bin]");
     run<4>(d_src, d_out, nb, ref, "V4 16x257 [sub][bin]");
+    run<5>(d_src, d_out, nb, ref, "V5 per-lane u8 [q][lane] + flush");
     return 0;
 }
