@@ -51,6 +51,16 @@ def parse():
     return ap.parse_args()
 
 
+def workload_name(args, n: int) -> str:
+    fmt = "fse_compress2" if args.nstates == 2 else "fse_compress"
+    gen = {0: "LUT", 1: "geometric", 2: "uniform"}.get(args.kind, f"kind {args.kind}")
+    c2 = (args.kind == 0 and args.prob == 0.155 and args.block == 65536 and n == 1 << 30)
+    tag = "C2" if c2 else "custom"
+    ent = " (H~4.02 bits/sym)" if c2 else ""
+    return (f"{tag}: {n / 2**30:g} GiB per GPU as {-(-n // args.block)} x {args.block // 1024} KiB independent "
+            f"blocks, {gen} generator p={args.prob}{ent}, encode ({fmt}-exact) + decode")
+
+
 def cpu_baseline(src_host: np.ndarray, block: int, budget_s: float) -> dict:
     """The parity oracle (C restatement of the reference, -O3) on host cores.
 
@@ -208,7 +218,7 @@ def main():
         torch.cuda.synchronize(dev)
         c3_ms = e3[0].elapsed_time(e3[1]) / args.steps
         c3_ok = int(dstat.abs().max()) == 0 and bool(torch.equal(out, src))
-        c3 = {"workload": "C3-style decode only on the C2 blocks above (prebuilt decode tables, untimed): "
+        c3 = {"workload": "C3-style decode only on the blocks above (prebuilt decode tables, untimed): "
                           f"{comp_bytes_pre / 2**30:.3f} GiB compressed -> {n / 2**30:.3f} GiB",
               "decode_ms": round(c3_ms, 4), "decode_GiB_s": round(n / (c3_ms * 1e-3) / 2**30, 2),
               "roofline_frac": None, "verified": c3_ok}
@@ -291,9 +301,7 @@ def main():
             "dtype": "u8",
             "data": "synthetic",
             "config": {
-                "workload": "C2: 1 GiB per GPU as 16384 x 64 KiB independent blocks, LUT generator "
-                            f"p={args.prob} (H~4.02 bits/sym), encode "
-                            f"({'fse_compress2' if args.nstates == 2 else 'fse_compress'}-exact) + decode",
+                "workload": workload_name(args, n),
                 "format": "2-state (fse_compress2)" if args.nstates == 2 else "1-state (fse_compress)",
                 "block_size": args.block,
                 "table_log": args.table_log or "optimal (11)",

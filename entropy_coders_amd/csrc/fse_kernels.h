@@ -49,6 +49,8 @@ struct DecParams {
     uint32_t variant;       // LDS layout / reader: 3/5 = padded image (prebuilt tables), else linear window
     uint32_t dual;          // two segments per lane, interleaved (prebuilt-table kernel)
     uint32_t stage_kib;     // LDS image size of the prebuilt-table kernel: 44 (default), 40 or 36 KiB
+    uint32_t pass;          // prebuilt-table kernel: 0 = all blocks, 1 = defer blocks the stage cannot
+                            // hold (status FSE_DEFERRED), 2 = only the deferred blocks (big stage)
     uint32_t nstates;       // 2 = fse_compress2 blocks (default), 1 = fse_compress blocks
 };
 
@@ -73,6 +75,7 @@ struct GenParams {
 };
 
 constexpr int kStamps = 10;  // stamp slots per workgroup
+constexpr int32_t FSE_DEFERRED = 1;  // internal block status between the two decode passes
 
 hipError_t launch_encode(const EncParams& P, uint32_t lmax, hipStream_t stream);
 hipError_t launch_dtables(const DtParams& P, uint32_t lmax, hipStream_t stream);

@@ -1394,8 +1394,13 @@ __global__ __launch_bounds__(64 * NW) void decode_pre_kernel(DecParams P) {
     constexpr bool PADDED = VAR == 3 || VAR == 5;
     const bool in_lds = PADDED ? (pad_word(nwords) + 2u) * 4u <= PMAX : clen <= PMAX;
     FSE_STAMP(P, 0);
+    if (P.pass == 2 && P.status[gb] != FSE_DEFERRED) return;  // done by the first pass
     if (info < 0 || n < 2) {
         if (tid == 0) P.status[gb] = info < 0 ? info : FSE_ERR_LENGTH_MISMATCH;
+        return;
+    }
+    if (P.pass == 1 && !in_lds) {  // too big for this stage: the big-stage pass decodes it
+        if (tid == 0) P.status[gb] = FSE_DEFERRED;
         return;
     }
     const int32_t hdr_bits = (info & 0xFFFF) * 8;
@@ -1958,11 +1963,26 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
                 else if (P.variant == 6) go(decode_pre_kernel<11, 4, PP, 6>, 256);
                 else if (P.stage_kib == 40) go(decode_pre_kernel<11, 4, (40u << 10), 2>, 256);
                 else if (P.stage_kib == 36) go(decode_pre_kernel<11, 4, (36u << 10), 2>, 256);
-                else go(decode_pre_kernel<11, 4, PP, 2>, 256);
+                else {
+                    // blocks above the 44 KiB stage (e.g. near-uniform data, ~65 KB) are
+                    // deferred to a second launch with a 66 KiB stage (2 workgroups per CU)
+                    // instead of the global-memory reader
+                    DecParams P1 = P, P2 = P;
+                    P1.pass = 1;
+                    P2.pass = 2;
+                    hipLaunchKernelGGL((decode_pre_kernel<11, 4, PP, 2>), g, dim3(256), 0, stream, P1);
+                    hipLaunchKernelGGL((decode_pre_kernel<11, 4, (66u << 10), 2>), g, dim3(256), 0, stream, P2);
+                }
             } else {
                 if (P.variant == 3) go(decode_pre_kernel<12, 4, PP - 8192, 3>, 256);
                 else if (P.variant == 5) go(decode_pre_kernel<12, 4, PP - 8192, 5>, 256);
-                else go(decode_pre_kernel<12, 4, PP - 8192, 2>, 256);
+                else {
+                    DecParams P1 = P, P2 = P;
+                    P1.pass = 1;
+                    P2.pass = 2;
+                    hipLaunchKernelGGL((decode_pre_kernel<12, 4, PP - 8192, 2>), g, dim3(256), 0, stream, P1);
+                    hipLaunchKernelGGL((decode_pre_kernel<12, 4, (66u << 10), 2>), g, dim3(256), 0, stream, P2);
+                }
             }
         }
         return hipGetLastError();
