@@ -1934,10 +1934,17 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
             if (!P.sidecar) {  // reference mode: serial, every read checked
                 if (lmax <= 11) go(decode1_serial_kernel<11>, 64);
                 else go(decode1_serial_kernel<12>, 64);
-            } else if (lmax <= 11) {
-                go(decode_pre_kernel<11, 4, PP, 2, 1>, 256);
-            } else {
-                go(decode_pre_kernel<12, 4, PP - 8192, 2, 1>, 256);
+            } else {  // two passes, as for 2-state blocks below
+                DecParams P1 = P, P2 = P;
+                P1.pass = 1;
+                P2.pass = 2;
+                if (lmax <= 11) {
+                    hipLaunchKernelGGL((decode_pre_kernel<11, 4, PP, 2, 1>), g, dim3(256), 0, stream, P1);
+                    hipLaunchKernelGGL((decode_pre_kernel<11, 4, (66u << 10), 2, 1>), g, dim3(256), 0, stream, P2);
+                } else {
+                    hipLaunchKernelGGL((decode_pre_kernel<12, 4, PP - 8192, 2, 1>), g, dim3(256), 0, stream, P1);
+                    hipLaunchKernelGGL((decode_pre_kernel<12, 4, (66u << 10), 2, 1>), g, dim3(256), 0, stream, P2);
+                }
             }
             return hipGetLastError();
         }

@@ -1,0 +1,82 @@
+"""GPU parity for the decode stage split (decode_pre_kernel
+"Oversized blocks"): blocks whose compressed image exceeds the 44 KiB LDS
+stage are deferred by the first launch and decoded by a 66 KiB-stage second
+launch; blocks above that use the global-memory reader. A batch that mixes
+all three kinds must still decode every block bit-exact, in both formats, and
+the encoded bytes must equal the oracle's (lib.rs:112-143, lib.rs:148-185).
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def _mixed_src(torch, codec, layout, seed=0x5EED0777):
+    """One block per (kind, prob) in `layout`, each from its own generator."""
+    parts = []
+    for i, (kind, prob) in enumerate(layout):
+        blk = codec.generate(kind, prob, seed + i, codec.block_size)
+        parts.append(blk)
+    return torch.cat(parts)
+
+
+def _check(torch, codec, src, n_check):
+    cb = codec.compress(src)
+    outs = [codec.decompress(cb), codec.decompress(cb, use_sidecar=False)]
+    tabs = codec.build_dtables(cb)
+    out3 = torch.empty_like(src)
+    st3 = torch.zeros(codec.n_blocks(src.numel()), dtype=torch.int32, device=codec.device)
+    codec.decompress_dt_into(cb, tabs, out3, st3)
+    outs.append((out3, st3))
+    torch.cuda.synchronize()
+    assert int(cb["status"].abs().max()) == 0
+    for out, st in outs:
+        assert int(st.abs().max()) == 0, st.cpu().numpy()
+        assert torch.equal(out, src)
+    host = src.cpu().numpy()
+    bs = codec.block_size
+    comp = O.compress2 if codec.nstates == 2 else O.compress
+    lens = cb["comp_len"].cpu().numpy()
+    for b in range(n_check):
+        want, wbits = comp(host[b * bs:(b + 1) * bs])
+        assert codec.block_bytes(cb, b) == want, f"block {b}"
+        assert int(cb["payload_bits"][b]) == wbits
+    return lens
+
+
+# uniform (~65 KB compressed: second pass), skewed (~8 KB: first pass), C2 (~33 KB)
+LAYOUT = [(2, 0.0), (0, 0.77), (0, 0.155), (2, 0.0), (2, 0.0), (0, 0.155), (1, 0.5), (2, 0.0)]
+
+
+@pytest.mark.parametrize("nstates", [2, 1])
+def test_mixed_stage_batch(torch_cuda, nstates):
+    from entropy_coders_amd import BlockCodec
+
+    codec = BlockCodec(block_size=65536, ckpt_interval=128 if nstates == 2 else 64, nstates=nstates)
+    src = _mixed_src(torch_cuda, codec, LAYOUT * 4)
+    lens = _check(torch_cuda, codec, src, len(LAYOUT))
+    assert (lens > 44 << 10).any() and (lens < 44 << 10).any()
+
+
+@pytest.mark.parametrize("nstates", [2, 1])
+def test_blocks_above_big_stage(torch_cuda, nstates):
+    """128 KiB blocks: uniform ones exceed even the 66 KiB stage (global
+    reader), skewed ones fit the 44 KiB stage."""
+    from entropy_coders_amd import BlockCodec
+
+    codec = BlockCodec(block_size=131072, ckpt_interval=128 if nstates == 2 else 64, nstates=nstates)
+    src = _mixed_src(torch_cuda, codec, [(2, 0.0), (0, 0.77), (0, 0.155), (2, 0.0)])
+    lens = _check(torch_cuda, codec, src, 4)
+    assert lens.max() > 66 << 10
+    assert np.count_nonzero(lens > 66 << 10) == 2
