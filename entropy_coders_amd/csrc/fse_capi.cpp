@@ -61,7 +61,7 @@ void* scratch(void* stream, int tag, uint64_t bytes) {
     }
     return w->ptr;
 }
-enum { SCRATCH_DT = 1, SCRATCH_DTINFO = 2 };
+enum { SCRATCH_DT = 1, SCRATCH_DTINFO = 2, SCRATCH_ENC = 3 };
 
 // Tuning / ablation knobs (not part of the ABI): FSEHIP_ENC_LANES=32|64,
 // FSEHIP_DEBUG bit mask (see fse_kernels.h).
@@ -284,6 +284,26 @@ int fsehip_compress_blocks(const fsehip_params* p, const uint8_t* d_src, uint64_
     P.status = d_status;
     P.lanes = (ns == 2 && env_u32("FSEHIP_ENC_LANES", 64) == 32) ? 32 : 64;
     P.debug = env_u32("FSEHIP_DEBUG", 0);
+    // scratch-path lane streams: worst case of a lane's steps at L = lmax,
+    // plus the top lane's extra step and lane 0's finals + marker, in whole
+    // 128-byte lines so no two lanes share a cache line
+    // (measured slower than the repair path on C2, skewed and uniform data:
+    // opt-in, FSEHIP_ENC_PATH=2 or 0 = by distribution)
+    P.path = env_u32("FSEHIP_ENC_PATH", 1);
+    P.warm = env_u32("FSEHIP_ENC_WARM", 64);
+    P.pmax256 = env_u32("FSEHIP_ENC_PMAX", 128);
+    P.scratch = nullptr;
+    if (P.path != 1 && P.lanes == 64 && ns == 2) {
+        const uint64_t steps = ns == 2 ? (bs >= 2 ? bs / 2 - 1 : 1) : (bs >= 1 ? bs - 1 : 1);
+        const uint64_t spc = ns == 2 ? 8 : 16;
+        uint64_t S = (steps + P.lanes - 1) / P.lanes;
+        S = std::max<uint64_t>(spc, (S + spc - 1) / spc * spc);
+        const uint64_t maxbits = S * ns * lmax + 3ull * lmax + 1;
+        P.scr_lane_words = (uint32_t)round_up((maxbits + 31) / 32 + 1, 32);
+        P.scratch = static_cast<uint32_t*>(
+            scratch(stream, SCRATCH_ENC, n_blocks * P.lanes * (uint64_t)P.scr_lane_words * 4u));
+        if (!P.scratch) return FSE_ERR_HIP;
+    }
     const size_t groups = (n_blocks * P.lanes + 63) / 64;
     P.stamps = g_stamps_enc.get(groups);
     hipError_t e = fsehip::launch_encode(P, lmax, static_cast<hipStream_t>(stream));

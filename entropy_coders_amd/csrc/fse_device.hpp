@@ -93,15 +93,13 @@ __device__ inline uint32_t wave_histogram(const uint8_t* __restrict__ src, uint3
     uint32_t* mine = hs + (lane % HSUB);
     uint32_t done = 0;
     if ((reinterpret_cast<uintptr_t>(src) & 15u) == 0) {
-        // 8 x 16-byte loads in flight per lane, then count them
+        // batches of 8 x 16-byte loads per lane, double-buffered: the next
+        // batch is in flight while the current one is counted
         constexpr uint32_t U = 8;
         const uint32_t nvec = n >> 4;
         const uint4* v4 = reinterpret_cast<const uint4*>(src);
         uint32_t v = 0;
-        for (; v + U * WAVE <= nvec; v += U * WAVE) {
-            uint4 d[U];
-#pragma unroll
-            for (uint32_t u = 0; u < U; ++u) d[u] = v4[v + u * WAVE + lane];
+        auto count = [&](const uint4* d) {
 #pragma unroll
             for (uint32_t u = 0; u < U; ++u) {
                 const uint32_t w[4] = {d[u].x, d[u].y, d[u].z, d[u].w};
@@ -111,6 +109,21 @@ __device__ inline uint32_t wave_histogram(const uint8_t* __restrict__ src, uint3
                     for (int b = 0; b < 4; ++b) atomicAdd(&mine[((w[k] >> (8 * b)) & 0xFFu) * HSUB], 1u);
                 }
             }
+        };
+        if (U * WAVE <= nvec) {
+            uint4 d[U];
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) d[u] = v4[u * WAVE + lane];
+            for (; v + 2u * U * WAVE <= nvec; v += U * WAVE) {
+                uint4 e[U];
+#pragma unroll
+                for (uint32_t u = 0; u < U; ++u) e[u] = v4[v + U * WAVE + u * WAVE + lane];
+                count(d);
+#pragma unroll
+                for (uint32_t u = 0; u < U; ++u) d[u] = e[u];
+            }
+            count(d);
+            v += U * WAVE;
         }
         for (v += lane; v < nvec; v += WAVE) {
             uint4 d = v4[v];
@@ -686,7 +699,10 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
     const uint32_t total_pos = __shfl(ex_p + sum_p, 63, 64);
     if (total_pos + total_neg > size || total_neg > size) return FSE_ERR_BAD_TABLE;
     const int32_t ht = (int32_t)size - 1 - (int32_t)total_neg;
-    for (uint32_t i = lane; i < size; i += WAVE) { occ_sym[i] = 0; sym_at[i] = 0; }
+    for (uint32_t i = lane; i < size / 16u; i += WAVE) {  // size >= 32: whole 16-byte stores
+        reinterpret_cast<uint4*>(occ_sym)[i] = make_uint4(0, 0, 0, 0);
+        reinterpret_cast<uint4*>(sym_at)[i] = make_uint4(0, 0, 0, 0);
+    }
     for (uint32_t s = lane; s < 256; s += WAVE) cnt[s] = 0;
     wave_sync();
     {

@@ -24,6 +24,15 @@ struct EncParams {
     uint32_t nstates;  // 2 = fse_compress2 (default), 1 = fse_compress
     uint32_t debug;  // ablation: bit0 = tables only, bit1 = no emit pass, bit2 = no payload stores
     uint64_t* stamps;  // diagnostics: per-workgroup s_memtime at phase ends
+    // Scratch-emit path (see encode_blocks_kernel): each lane writes its
+    // bits to a lane-private scratch stream from the start state the count
+    // pass gives it, and a copy pass moves the streams to their final bit
+    // offsets once the exact lengths are known.  nullptr = repair path only.
+    uint32_t* scratch;        // [n_blocks][lanes][scr_lane_words]
+    uint32_t scr_lane_words;  // words per lane stream (worst case, multiple of 32)
+    uint32_t warm;            // count-pass warm-up pairs above the lane's range (scratch path)
+    uint32_t path;            // 0 = by distribution, 1 = repair path, 2 = scratch path
+    uint32_t pmax256;         // auto: scratch path when max norm <= pmax256/256 of the table
 };
 
 struct DecParams {

@@ -162,7 +162,9 @@ struct Ckpt {
     uint32_t L;
 };
 
-enum { PASS_SPEC = 0, PASS_COUNT = 1, PASS_EMIT = 2, PASS_REPAIR = 3 };
+// PASS_STATE: state chain only (the scratch path's count pass, no bits and
+// no trajectory).
+enum { PASS_STATE = 0, PASS_COUNT = 1, PASS_EMIT = 2, PASS_REPAIR = 3 };
 
 // Trajectory of a count pass, for convergence-based repair: the state pair
 // and running bit count after every ckc-th chunk (at most TRACK_SLOTS slots per lane,
@@ -397,8 +399,8 @@ struct EncSmem {
             union {
                 uint32_t hs[HIST_WORDS];  // sub-histograms (counts[] go to cnt[], free until the spread)
                 struct {
-                    uint8_t sym_at[SIZE];
-                    uint8_t occ_sym[SIZE];
+                    __attribute__((aligned(16))) uint8_t sym_at[SIZE];
+                    __attribute__((aligned(16))) uint8_t occ_sym[SIZE];
                 } sp;
             } u;
             int32_t norm[256];
@@ -412,17 +414,19 @@ struct EncSmem {
                                           // aligned, conflict-free dwordx4 reads)
             } u;
             uint32_t cntF[BPW][T + 1];
+            uint32_t emF[BPW][T + 1];  // scratch path: end states of the emit pass
             uint32_t mword[BPW][2 * (T + 1)];
             uint32_t mval[BPW][2 * (T + 1)];
         } p2;
     } ph;
     int32_t info_status[BPW];
+    uint32_t info_new[BPW];  // block takes the scratch path
     uint32_t info_L[BPW];
     uint32_t info_hl[BPW];
     int scratch[4];
 };
 
-template <int LMAX, int T, int NS>
+template <int LMAX, int T, int NS, bool SCR = false>
 __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     constexpr int BPW = 64 / T;
     __shared__ EncSmem<LMAX, T> sm;
@@ -433,7 +437,10 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     for (int b = 0; b < BPW; ++b) {
         const uint64_t gb = (uint64_t)blockIdx.x * BPW + b;
         if (gb >= P.n_blocks) {
-            if (lane == 0) sm.info_status[b] = 1;  // no block
+            if (lane == 0) {
+                sm.info_status[b] = 1;  // no block
+                sm.info_new[b] = 1u;
+            }
             continue;
         }
         const uint64_t off = gb * P.block_size;
@@ -453,6 +460,17 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
         if (rc == FSE_OK) rc = wave_normalize(counts, n, tl, Lreq, sm.ph.p1.norm, &L, &slow, sm.scratch);
         if (rc == FSE_OK && n < 2) rc = FSE_ERR_TOO_SHORT;  // lib.rs:154/156 unwrap
         if (rc == FSE_OK && L > (uint32_t)LMAX) rc = FSE_ERR_UNSUPPORTED;
+        // scratch path unless the distribution is skewed (its encoder
+        // trajectories merge slowly, so start states from the count pass
+        // would often be wrong and every wrong one costs a whole re-emit)
+        bool newp = SCR && P.scratch != nullptr && P.path != 1u;
+        if (newp && P.path == 0u && rc == FSE_OK) {
+            uint32_t mx = 0;
+            for (uint32_t s = lane; s < tl; s += WAVE) mx = max(mx, (uint32_t)max(sm.ph.p1.norm[s], 0));
+            mx = wave_max(mx);
+            newp = (uint64_t)mx * 256u <= ((uint64_t)P.pmax256 << L);
+        }
+        if (lane == 0) sm.info_new[b] = newp ? 1u : 0u;
         FSE_STAMP(P, 2);
         if (rc == FSE_OK) {
             const int hl = wave_header_write(sm.ph.p1.norm, L, tl, sm.hdrw[b]);
@@ -525,46 +543,132 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     em.start(nullptr, 0);
     Ckpt ck{nullptr, 0, 0, 0, L};
 
-    // count pass: the top lane from its exact start (init states + the
-    // odd-length extra step), every other lane from a guessed start state,
-    // recording its trajectory.  Then verify against the neighbour's end
-    // state and repair by convergence (Track) until the fixed point.
+    // Two ways to the exact start state of every lane (the lane above's end
+    // state) and the exact bit offset of every lane:
+    //  * repair path: count pass from guessed starts with trajectories, then
+    //    convergence repair (re-encode from the corrected start until the
+    //    recorded trajectory is met) until the fixed point, then the emit
+    //    pass writes straight to the final offsets.  A repair round costs the
+    //    slowest lane's convergence distance.
+    //  * scratch path: count pass (state chains only, from a guessed start
+    //    `warm` pairs above the lane's range), then the emit pass from those
+    //    end states into lane-private scratch streams, which also yields the
+    //    exact lengths.  A lane's start was right iff the emit end state of
+    //    the lane above equals the count end state it was given (by
+    //    induction from the exact top lane); a wrong one re-emits.  A copy
+    //    pass then moves every stream to its final bit offset.
+    bool newp = SCR;
+#pragma unroll
+    for (int bb = 0; bb < BPW; ++bb) newp = newp && sm.info_new[bb] != 0u;  // wave-uniform
     Track tr{&sm.ph.p2.u.cp[lane * TRACK_SLOTS], max(1u, (S / SPC + TRACK_SLOTS - 1u) / TRACK_SLOTS), false, 0u};
     const uint32_t nslot = pb > pa ? (((pb - 1u) / SPC) - (pa / SPC)) / tr.ckc + 1u : 0u;
     uint32_t start = (1u << L) | (NS == 2 ? (1u << L) << 16 : 0u);
     uint32_t bits = 0;
-    if (act) {
-        EncState e0 = (k == ktop) ? top_start<PASS_COUNT, NS>(blk, n, tab, em) : EncState{start & 0xFFFFu, start >> 16, 0u};
-        e0 = enc_range<PASS_COUNT, NS>(blk, n, pa, pb, e0, tab, em, ck, tr);
-        bits = e0.bits;
-        sm.ph.p2.cntF[b][k] = e0.x0 | (e0.x1 << 16);
-        track_fixup(tr, nslot, -1, bits);
-    }
-    FSE_STAMP(P, 5);
+    uint32_t* sw = nullptr;  // scratch path: this lane's stream
     uint32_t n_iter = 0, n_rerun = 0;  // diagnostics (stamps counters)
-    for (;;) {
-        __syncthreads();
-        bool bad = false;
-        uint32_t nbF = 0;
-        if (act && k < ktop) {
-            nbF = sm.ph.p2.cntF[b][k + 1];
-            bad = nbF != start;
+    if (newp) {
+        sw = P.scratch + ((uint64_t)gb * T + k) * P.scr_lane_words;
+        if (act) {
+            EncState e0;
+            uint32_t ptop = pb;
+            if (k == ktop) {
+                e0 = top_start<PASS_STATE, NS>(blk, n, tab, em);
+            } else {
+                e0 = EncState{start & 0xFFFFu, start >> 16, 0u};
+                ptop = min(pb + P.warm, Pm);
+            }
+            e0 = enc_range<PASS_STATE, NS>(blk, n, pa, ptop, e0, tab, em, ck, tr);
+            sm.ph.p2.cntF[b][k] = e0.x0 | (e0.x1 << 16);
         }
+        FSE_STAMP(P, 5);
         __syncthreads();
-        if (__ballot(bad) == 0) break;
-        ++n_iter;
-        n_rerun += (uint32_t)__popcll(__ballot(bad));
-        if (bad) {
-            start = nbF;
-            tr.done = false;
-            const EncState e0 = enc_range<PASS_REPAIR, NS>(blk, n, pa, pb, EncState{start & 0xFFFFu, start >> 16, 0u},
-                                                       tab, em, ck, tr);
+        if (act && k < ktop) start = sm.ph.p2.cntF[b][k + 1];
+        Ckpt ckl{nullptr, 0, 0, 0, L};
+        if (P.sidecar && P.ckpt_interval) {
+            ckl.base = P.sidecar + gb * P.ckpt_per_block;
+            ckl.mask = P.ckpt_interval - 1u;
+            ckl.shift = 31u - __clz(P.ckpt_interval);
+            ckl.hdr_bits = 0;  // lane-local positions until the copy pass
+        }
+        // the lane's whole stream (including the finals and marker of lane 0)
+        // into its scratch words; checkpoints at lane-local bit positions
+        auto emit_lane = [&]() -> uint32_t {
+            em.start(sw, 0, P.scr_lane_words, &sm.ph.p2.u.ring[lane * 36u]);
+            EncState e0;
+            if (k == ktop) {
+                e0 = top_start<PASS_EMIT, NS>(blk, n, tab, em);
+                if (ckl.base && (Pm & ckl.mask) == 0u) ckpt_record<NS>(ckl, Pm, em.pos(), e0.x0, e0.x1);
+            } else {
+                e0 = EncState{start & 0xFFFFu, start >> 16, 0u};
+            }
+            e0 = enc_range<PASS_EMIT, NS>(blk, n, pa, pb, e0, tab, em, ckl, tr);
+            sm.ph.p2.emF[b][k] = e0.x0 | (e0.x1 << 16);
+            if (k == 0) {  // Encoder::finish (x2 for NS = 2) + marker (lib.rs:178-181 / 139-141)
+                const uint32_t m = (1u << L) - 1u;
+                if (NS == 2) {
+                    em.put(e0.x1 & m, L);
+                    em.flush();
+                }
+                em.put(e0.x0 & m, L);
+                em.flush();
+                em.put(1u, 1u);
+                em.flush();
+            }
+            em.finish();
+            if (em.nacc) sw[em.word] = em.lo;  // the partial last word (lane-private)
+            return em.pos();
+        };
+        if (act) bits = emit_lane();
+        for (;;) {
+            __syncthreads();
+            const bool bad = act && k < ktop && sm.ph.p2.emF[b][k + 1] != start;
+            __syncthreads();
+            if (__ballot(bad) == 0) break;
+            ++n_iter;
+            n_rerun += (uint32_t)__popcll(__ballot(bad));
+            if (bad) {
+                start = sm.ph.p2.emF[b][k + 1];
+                bits = emit_lane();
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // scratch and sidecar stores land before the copy reads
+    } else {
+        // count pass: the top lane from its exact start (init states + the
+        // odd-length extra step), every other lane from a guessed start state,
+        // recording its trajectory.  Then verify against the neighbour's end
+        // state and repair by convergence (Track) until the fixed point.
+        if (act) {
+            EncState e0 = (k == ktop) ? top_start<PASS_COUNT, NS>(blk, n, tab, em) : EncState{start & 0xFFFFu, start >> 16, 0u};
+            e0 = enc_range<PASS_COUNT, NS>(blk, n, pa, pb, e0, tab, em, ck, tr);
             bits = e0.bits;
-            if (!tr.done) sm.ph.p2.cntF[b][k] = e0.x0 | (e0.x1 << 16);  // did not converge: new end state
-            track_fixup(tr, nslot, tr.done ? (int32_t)tr.jstar : -1, bits);
+            sm.ph.p2.cntF[b][k] = e0.x0 | (e0.x1 << 16);
+            track_fixup(tr, nslot, -1, bits);
         }
+        FSE_STAMP(P, 5);
+        for (;;) {
+            __syncthreads();
+            bool bad = false;
+            uint32_t nbF = 0;
+            if (act && k < ktop) {
+                nbF = sm.ph.p2.cntF[b][k + 1];
+                bad = nbF != start;
+            }
+            __syncthreads();
+            if (__ballot(bad) == 0) break;
+            ++n_iter;
+            n_rerun += (uint32_t)__popcll(__ballot(bad));
+            if (bad) {
+                start = nbF;
+                tr.done = false;
+                const EncState e0 = enc_range<PASS_REPAIR, NS>(blk, n, pa, pb, EncState{start & 0xFFFFu, start >> 16, 0u},
+                                                           tab, em, ck, tr);
+                bits = e0.bits;
+                if (!tr.done) sm.ph.p2.cntF[b][k] = e0.x0 | (e0.x1 << 16);  // did not converge: new end state
+                track_fixup(tr, nslot, tr.done ? (int32_t)tr.jstar : -1, bits);
+            }
+        }
+        if (k == 0) bits += (uint32_t)NS * L + 1u;  // finals + marker (lib.rs:178-181 / 139-141)
     }
-    if (k == 0) bits += (uint32_t)NS * L + 1u;  // finals + marker (lib.rs:178-181 / 139-141)
 
     FSE_STAMP(P, 6);
     if (P.stamps && lane == 0)
@@ -584,7 +688,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     const bool fits = (uint64_t)total_bits <= P.slot_bytes * 8ull && !(P.debug & 2u);
     uint32_t* gw = reinterpret_cast<uint32_t*>(P.out + gb * P.slot_bytes);
 
-    // emit pass
+    // emit pass (repair path) or copy pass (scratch path)
     for (uint32_t e = k; e < 2u * (T + 1u); e += T) {
         if (b < BPW) sm.ph.p2.mword[b][e] = 0xFFFFFFFFu;
     }
@@ -592,32 +696,88 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     if (act && fits) {
         em.start(gw, off, (P.debug & 4u) ? 0u : (uint32_t)(P.slot_bytes >> 2),  // debug bit 2: no payload stores (ablation)
                  &sm.ph.p2.u.ring[lane * 36u]);
-        if (P.sidecar && P.ckpt_interval) {
-            ck.base = P.sidecar + gb * P.ckpt_per_block;
-            ck.mask = P.ckpt_interval - 1u;
-            ck.shift = 31u - __clz(P.ckpt_interval);
-            ck.hdr_bits = hdr_bits;
-        }
-        EncState e0;
-        if (k == ktop) {
-            e0 = top_start<PASS_EMIT, NS>(blk, n, tab, em);
-            if (ck.base && (Pm & ck.mask) == 0u)  // checkpoint "before step Pm"
-                ckpt_record<NS>(ck, Pm, em.pos(), e0.x0, e0.x1);
-        } else {
-            e0 = EncState{start & 0xFFFFu, start >> 16, 0u};
-        }
-        e0 = enc_range<PASS_EMIT, NS>(blk, n, pa, pb, e0, tab, em, ck, tr);
-        const uint32_t y0 = e0.x0, y1 = e0.x1;
-        if (k == 0) {  // Encoder::finish (x2 for NS = 2) + marker (lib.rs:178-181 / 139-141)
-            const uint32_t m = (1u << L) - 1u;
-            if (NS == 2) {
-                em.put(y1 & m, L);
+        if (newp) {
+            // the lane's stream at its final offset: whole words through the
+            // emitter (ring, 64-byte groups, merge list), then the tail bits
+            // (four 16-byte loads in flight ahead of the words being moved)
+            const uint32_t nw = bits >> 5, rb = bits & 31u, nq = nw >> 2;
+            const uint4* s4 = reinterpret_cast<const uint4*>(sw);
+            auto put4 = [&](const uint4& q) {
+                em.put(q.x, 32u);
+                em.flush();
+                em.put(q.y, 32u);
+                em.flush();
+                em.put(q.z, 32u);
+                em.flush();
+                em.put(q.w, 32u);
+                em.flush();
+                em.drain();
+            };
+            if (nq) {
+                auto ldq = [&](uint32_t q) { return s4[min(q, nq - 1u)]; };
+                uint4 c0 = ldq(0), c1 = ldq(1), c2 = ldq(2), c3 = ldq(3);
+                for (uint32_t q = 0; q < nq; q += 4u) {
+                    const uint4 n0 = ldq(q + 4u), n1 = ldq(q + 5u), n2 = ldq(q + 6u), n3 = ldq(q + 7u);
+                    put4(c0);
+                    if (q + 1u < nq) put4(c1);
+                    if (q + 2u < nq) put4(c2);
+                    if (q + 3u < nq) put4(c3);
+                    c0 = n0;
+                    c1 = n1;
+                    c2 = n2;
+                    c3 = n3;
+                }
+            }
+            for (uint32_t i = nq << 2; i < nw; ++i) {
+                em.put(sw[i], 32u);
                 em.flush();
             }
-            em.put(y0 & m, L);
-            em.flush();
-            em.put(1u, 1u);
-            em.flush();
+            em.drain();
+            if (rb) {
+                em.put(sw[nw] & ((1u << rb) - 1u), rb);
+                em.flush();
+            }
+            // sidecar: lane-local positions -> payload-relative ones
+            if (P.sidecar && P.ckpt_interval) {
+                uint64_t* base = P.sidecar + gb * P.ckpt_per_block;
+                const uint32_t I = P.ckpt_interval;
+                const uint32_t i0 = (pa + I - 1u) / I;
+                uint32_t i1 = (pb + I - 1u) / I;
+                if (k == ktop && (Pm & (I - 1u)) == 0u) i1 = Pm / I + 1u;
+                const uint32_t delta = off - hdr_bits;
+                for (uint32_t j = i0; j < i1; ++j) {
+                    const uint64_t v = base[j];
+                    base[j] = (v & ~0xFFFFFFFFull) | (uint64_t)((uint32_t)v + delta);
+                }
+            }
+        } else {
+            if (P.sidecar && P.ckpt_interval) {
+                ck.base = P.sidecar + gb * P.ckpt_per_block;
+                ck.mask = P.ckpt_interval - 1u;
+                ck.shift = 31u - __clz(P.ckpt_interval);
+                ck.hdr_bits = hdr_bits;
+            }
+            EncState e0;
+            if (k == ktop) {
+                e0 = top_start<PASS_EMIT, NS>(blk, n, tab, em);
+                if (ck.base && (Pm & ck.mask) == 0u)  // checkpoint "before step Pm"
+                    ckpt_record<NS>(ck, Pm, em.pos(), e0.x0, e0.x1);
+            } else {
+                e0 = EncState{start & 0xFFFFu, start >> 16, 0u};
+            }
+            e0 = enc_range<PASS_EMIT, NS>(blk, n, pa, pb, e0, tab, em, ck, tr);
+            const uint32_t y0 = e0.x0, y1 = e0.x1;
+            if (k == 0) {  // Encoder::finish (x2 for NS = 2) + marker (lib.rs:178-181 / 139-141)
+                const uint32_t m = (1u << L) - 1u;
+                if (NS == 2) {
+                    em.put(y1 & m, L);
+                    em.flush();
+                }
+                em.put(y0 & m, L);
+                em.flush();
+                em.put(1u, 1u);
+                em.flush();
+            }
         }
         em.finish();
         // boundary words -> merge list (entry order = stream order)
@@ -1393,8 +1553,8 @@ __global__ __launch_bounds__(64 * NW) void decode_pre_kernel(DecParams P) {
     const uint32_t nwords = (clen + 3u) >> 2;
     constexpr bool PADDED = VAR == 3 || VAR == 5;
     const bool in_lds = PADDED ? (pad_word(nwords) + 2u) * 4u <= PMAX : clen <= PMAX;
-    FSE_STAMP(P, 0);
     if (P.pass == 2 && P.status[gb] != FSE_DEFERRED) return;  // done by the first pass
+    FSE_STAMP(P, 0);
     if (info < 0 || n < 2) {
         if (tid == 0) P.status[gb] = info < 0 ? info : FSE_ERR_LENGTH_MISMATCH;
         return;
@@ -1544,8 +1704,8 @@ __global__ __launch_bounds__(64) void dtable_blocks_kernel(DtParams P) {
     __shared__ int32_t norm[256];
     __shared__ uint16_t cumul[256];
     __shared__ uint32_t cnt[256];
-    __shared__ uint8_t sym_at[SIZE];
-    __shared__ uint8_t occ[SIZE];
+    __shared__ __attribute__((aligned(16))) uint8_t sym_at[SIZE];
+    __shared__ __attribute__((aligned(16))) uint8_t occ[SIZE];
     const uint32_t lane = lane_id();
     const uint64_t gb = blockIdx.x;
     if (gb >= P.n_blocks) return;
@@ -1908,6 +2068,9 @@ hipError_t launch_encode(const EncParams& P, uint32_t lmax, hipStream_t stream) 
     if (P.nstates == 1) {  // fse_compress (lib.rs:112-143)
         if (lmax <= 11) hipLaunchKernelGGL((encode_blocks_kernel<11, 64, 1>), g, b, 0, stream, P);
         else hipLaunchKernelGGL((encode_blocks_kernel<12, 64, 1>), g, b, 0, stream, P);
+    } else if (T == 64 && P.scratch) {  // scratch path built in (FSEHIP_ENC_PATH=0|2)
+        if (lmax <= 11) hipLaunchKernelGGL((encode_blocks_kernel<11, 64, 2, true>), g, b, 0, stream, P);
+        else hipLaunchKernelGGL((encode_blocks_kernel<12, 64, 2, true>), g, b, 0, stream, P);
     } else if (T == 64) {
         if (lmax <= 11) hipLaunchKernelGGL((encode_blocks_kernel<11, 64, 2>), g, b, 0, stream, P);
         else hipLaunchKernelGGL((encode_blocks_kernel<12, 64, 2>), g, b, 0, stream, P);
