@@ -292,6 +292,7 @@ int fsehip_compress_blocks(const fsehip_params* p, const uint8_t* d_src, uint64_
     P.path = env_u32("FSEHIP_ENC_PATH", 1);
     P.warm = env_u32("FSEHIP_ENC_WARM", 64);
     P.pmax256 = env_u32("FSEHIP_ENC_PMAX", 128);
+    P.xlds = env_u32("FSEHIP_ENC_XLDS", 0);
     P.scratch = nullptr;
     if (P.path != 1 && P.lanes == 64 && ns == 2) {
         const uint64_t steps = ns == 2 ? (bs >= 2 ? bs / 2 - 1 : 1) : (bs >= 1 ? bs - 1 : 1);

@@ -79,43 +79,63 @@ __device__ __forceinline__ uint64_t match_u8(uint32_t key, uint64_t active) {
 // pile onto one bank.  Measured against 4 copies at a 257-word stride
 // (tools/micro/hist_bench.hip, 1 GiB): C2 0.46 -> 0.29 ms, uniform
 // 0.24 -> 0.21 ms, LUT p=0.77 0.95 -> 0.43 ms.
+// Counters are 16-bit: a bin's 8 copies are 4 words of two halves (copy c =
+// lane % 8 counts in word c / 2, half c % 2), so the increment is a per-lane
+// constant and a byte's address is one shift-or; the encoder holds 4 KiB of
+// sub-histograms instead of 8.  A copy counts at most 1/8 of a segment's
+// bytes, so segments of HIST_SEG bytes cannot overflow a half; each segment
+// is folded into the u32 counts[].
 // Returns table_len (1 + largest symbol, 1 for an empty block).  counts
 // must not alias hs.
 // ---------------------------------------------------------------------------
 constexpr uint32_t HSUB = 8;
-constexpr uint32_t HIST_WORDS = HSUB * 256;
+constexpr uint32_t HIST_WORDS = 256 * HSUB / 2;
+constexpr uint32_t HIST_SEG = 1u << 18;
 
-__device__ inline uint32_t wave_histogram(const uint8_t* __restrict__ src, uint32_t n,
-                                          uint32_t* hs /*LDS [HIST_WORDS]*/, uint32_t* counts /*LDS[256]*/) {
+// The counting loop is a call of its own (noinline): inlined, it raised the
+// encoder's VGPR count from 119 to 210.  Across the call the pointers are
+// generic, so they are cast back to their address spaces here (a generic
+// sub-histogram pointer would make every increment a FLAT atomic).
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const u32x4 gbl_u4;
+typedef __attribute__((address_space(1))) const uint8_t gbl_u8;
+
+__device__ __attribute__((noinline)) void wave_histogram_seg(const uint8_t* __restrict__ src_generic, uint32_t n,
+                                                             uint32_t* hs_generic) {
     const uint32_t lane = lane_id();
-    for (uint32_t i = lane; i < HIST_WORDS; i += WAVE) hs[i] = 0;
-    wave_sync();
-    uint32_t* mine = hs + (lane % HSUB);
+    // byte address of this lane's copy: ((lane / 2) % 4) words into each bin's 4
+    lds_u32* mine = (lds_u32*)hs_generic + ((lane >> 1) & 3u);
+    const uint32_t inc = 1u << (16u * (lane & 1u));
+    gbl_u8* src = (gbl_u8*)src_generic;
+    auto add = [&](uint32_t byte) {
+        __hip_atomic_fetch_add(&mine[byte * 4u], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
     uint32_t done = 0;
-    if ((reinterpret_cast<uintptr_t>(src) & 15u) == 0) {
+    if ((reinterpret_cast<uintptr_t>(src_generic) & 15u) == 0) {
         // batches of 8 x 16-byte loads per lane, double-buffered: the next
         // batch is in flight while the current one is counted
         constexpr uint32_t U = 8;
         const uint32_t nvec = n >> 4;
-        const uint4* v4 = reinterpret_cast<const uint4*>(src);
+        gbl_u4* v4 = (gbl_u4*)src_generic;
         uint32_t v = 0;
-        auto count = [&](const uint4* d) {
+        auto count = [&](const u32x4* d) {
 #pragma unroll
             for (uint32_t u = 0; u < U; ++u) {
                 const uint32_t w[4] = {d[u].x, d[u].y, d[u].z, d[u].w};
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
 #pragma unroll
-                    for (int b = 0; b < 4; ++b) atomicAdd(&mine[((w[k] >> (8 * b)) & 0xFFu) * HSUB], 1u);
+                    for (int b = 0; b < 4; ++b) add((w[k] >> (8 * b)) & 0xFFu);
                 }
             }
         };
         if (U * WAVE <= nvec) {
-            uint4 d[U];
+            u32x4 d[U];
 #pragma unroll
             for (uint32_t u = 0; u < U; ++u) d[u] = v4[u * WAVE + lane];
             for (; v + 2u * U * WAVE <= nvec; v += U * WAVE) {
-                uint4 e[U];
+                u32x4 e[U];
 #pragma unroll
                 for (uint32_t u = 0; u < U; ++u) e[u] = v4[v + U * WAVE + u * WAVE + lane];
                 count(d);
@@ -126,26 +146,41 @@ __device__ inline uint32_t wave_histogram(const uint8_t* __restrict__ src, uint3
             v += U * WAVE;
         }
         for (v += lane; v < nvec; v += WAVE) {
-            uint4 d = v4[v];
-            uint32_t w[4] = {d.x, d.y, d.z, d.w};
+            const u32x4 d = v4[v];
+            const uint32_t w[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
 #pragma unroll
-                for (int b = 0; b < 4; ++b) atomicAdd(&mine[((w[k] >> (8 * b)) & 0xFFu) * HSUB], 1u);
+                for (int b = 0; b < 4; ++b) add((w[k] >> (8 * b)) & 0xFFu);
             }
         }
         done = nvec << 4;
     }
-    for (uint32_t i = done + lane; i < n; i += WAVE) atomicAdd(&mine[src[i] * HSUB], 1u);
-    wave_sync();
+    for (uint32_t i = done + lane; i < n; i += WAVE) add(src[i]);
+}
+
+__device__ inline uint32_t wave_histogram(const uint8_t* __restrict__ src, uint32_t n,
+                                          uint32_t* hs /*LDS [HIST_WORDS]*/, uint32_t* counts /*LDS[256]*/) {
+    const uint32_t lane = lane_id();
+    for (uint32_t s = lane; s < 256; s += WAVE) counts[s] = 0;
+    uint32_t seg = 0;
+    do {
+        for (uint32_t i = lane; i < HIST_WORDS; i += WAVE) hs[i] = 0;
+        wave_sync();
+        const uint32_t m = min(n - seg, HIST_SEG);
+        wave_histogram_seg(src + seg, m, hs);
+        wave_sync();
+        for (uint32_t s = lane; s < 256; s += WAVE) {
+            const uint4 q = reinterpret_cast<const uint4*>(hs)[s];
+            counts[s] += (q.x & 0xFFFFu) + (q.x >> 16) + (q.y & 0xFFFFu) + (q.y >> 16) + (q.z & 0xFFFFu) +
+                         (q.z >> 16) + (q.w & 0xFFFFu) + (q.w >> 16);
+        }
+        wave_sync();
+        seg += m;
+    } while (seg < n);
     uint32_t tl = 0;
-    for (uint32_t s = lane; s < 256; s += WAVE) {
-        uint32_t c = 0;
-#pragma unroll
-        for (uint32_t h = 0; h < HSUB; ++h) c += hs[s * HSUB + h];
-        counts[s] = c;
-        if (c) tl = max(tl, s + 1u);
-    }
+    for (uint32_t s = lane; s < 256; s += WAVE)
+        if (counts[s]) tl = max(tl, s + 1u);
     tl = wave_max(tl);
     wave_sync();
     return tl == 0 ? 1u : tl;

@@ -33,6 +33,7 @@ struct EncParams {
     uint32_t warm;            // count-pass warm-up pairs above the lane's range (scratch path)
     uint32_t path;            // 0 = by distribution, 1 = repair path, 2 = scratch path
     uint32_t pmax256;         // auto: scratch path when max norm <= pmax256/256 of the table
+    uint32_t xlds;            // diagnostics: extra dynamic LDS bytes per workgroup (occupancy probe)
 };
 
 struct DecParams {

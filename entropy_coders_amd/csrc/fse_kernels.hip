@@ -59,10 +59,13 @@ struct EncTab {
 // lane: the merge step later rewrites each boundary word with the OR of both
 // lanes' bits.
 // Bit writer of one lane's range: BitStackWriter order (writer.rs:140-222),
-// words through a 32-word LDS ring.  Every 16-word group of the slot that
-// lies wholly inside the lane's range leaves as one 64-byte store (four
-// dwordx4, a whole HBM burst) once the lane has moved past it; the partial
-// groups at either end leave as dword stores.  The lane's first word, when
+// words through a 16-word LDS ring (RING_STRIDE words per lane: 16-byte
+// aligned, conflict-free dwordx4 reads).  Every 8-word group of the slot
+// that lies wholly inside the lane's range leaves as one 32-byte store (two
+// dwordx4; L2 merges a lane's consecutive groups into whole lines) once the
+// lane has moved past it; the partial groups at either end leave as dword
+// stores.  (A 32-word ring with 64-byte groups needed 9 KiB of LDS per
+// workgroup, which held the encoder at 8 workgroups per CU.)  The lane's first word, when
 // it shares it with the lane above (off % 32 != 0), is never stored: its
 // value (head_val) goes to the merge list, like the lane's last partial
 // word.  Stores stay below wlim (the slot's words).
@@ -73,10 +76,10 @@ struct Emit {
     uint32_t w0;        // first word index of the lane
     uint32_t head_val;  // lane's bits of word w0 (valid once word > w0 and the head group left)
     uint32_t wlim;      // words in the slot: stores never leave it
-    uint32_t gs;        // next 16-word group to store
+    uint32_t gs;        // next 8-word group to store
     bool skip_head;
     uint32_t* gw;
-    uint32_t* ring;     // LDS, 32 words, 16-byte aligned
+    uint32_t* ring;     // LDS, 16 words, 16-byte aligned
     __device__ __forceinline__ void start(uint32_t* g, uint32_t off, uint32_t lim = 0xFFFFFFFFu,
                                           uint32_t* r = nullptr) {
         gw = g;
@@ -86,7 +89,7 @@ struct Emit {
         nacc = off & 31u;
         word = off >> 5;
         w0 = word;
-        gs = word >> 4;
+        gs = word >> 3;
         skip_head = (off & 31u) != 0u;
         head_val = 0;
     }
@@ -101,7 +104,7 @@ struct Emit {
     // flush before nacc can reach 64 (<= 2 x 12 bits per flush).
     __device__ __forceinline__ void flush() {
         const bool f = nacc >= 32u;
-        ring[word & 31u] = lo;
+        ring[word & 15u] = lo;
         lo = f ? hi : lo;
         hi = 0;  // nacc < 32 after the flush
         nacc &= 31u;
@@ -110,27 +113,26 @@ struct Emit {
     __device__ __forceinline__ uint32_t pos() const { return word * 32u + nacc; }
     __device__ __forceinline__ void store_words(uint32_t a, uint32_t b) {
         for (uint32_t i = a; i < b; ++i)
-            if (i < wlim) gw[i] = ring[i & 31u];
+            if (i < wlim) gw[i] = ring[i & 15u];
     }
     __device__ __forceinline__ void store_group(uint32_t g) {
-        const uint32_t base = g << 4;
-        if (g == (w0 >> 4) && ((w0 & 15u) != 0u || skip_head)) {  // the lane's first group: its own words only
-            if (skip_head) head_val = ring[w0 & 31u];
-            store_words(skip_head ? w0 + 1u : w0, base + 16u);
-        } else if (base + 16u <= wlim) {
-            const uint4* r = reinterpret_cast<const uint4*>(ring + (base & 31u));
+        const uint32_t base = g << 3;
+        if (g == (w0 >> 3) && ((w0 & 7u) != 0u || skip_head)) {  // the lane's first group: its own words only
+            if (skip_head) head_val = ring[w0 & 15u];
+            store_words(skip_head ? w0 + 1u : w0, base + 8u);
+        } else if (base + 8u <= wlim) {
+            const uint4* r = reinterpret_cast<const uint4*>(ring + (base & 15u));
             uint4* o = reinterpret_cast<uint4*>(gw + base);
-            const uint4 a = r[0], b = r[1], c = r[2], d = r[3];
+            const uint4 a = r[0], b = r[1];
             o[0] = a;
             o[1] = b;
-            o[2] = c;
-            o[3] = d;
         }
     }
     // Store the group the lane has moved past, if any (called every <= 8
-    // pairs: <= 6 new words, so the ring never overruns a pending group).
+    // pairs: <= 6 new words, fewer than a group, so the ring never overruns
+    // a pending group and at most one group completes between calls).
     __device__ __forceinline__ void drain() {
-        if (word >= (gs + 1u) << 4) {
+        if (word >= (gs + 1u) << 3) {
             store_group(gs);
             ++gs;
         }
@@ -138,21 +140,25 @@ struct Emit {
     // End of the lane: remaining whole groups, then the whole words of the
     // last group (the partial word stays in acc for the merge list).
     __device__ __forceinline__ void finish() {
-        while (word >= (gs + 1u) << 4) {
+        while (word >= (gs + 1u) << 3) {
             store_group(gs);
             ++gs;
         }
-        uint32_t lo = gs << 4;
-        if (gs == (w0 >> 4)) {
+        uint32_t lo = gs << 3;
+        if (gs == (w0 >> 3)) {
             lo = w0;
             if (skip_head) {
                 lo = w0 + 1u;
-                if (word > w0) head_val = ring[w0 & 31u];
+                if (word > w0) head_val = ring[w0 & 15u];
             }
         }
         store_words(lo, word);
     }
 };
+
+// Words per lane of the emit ring in LDS: 16 used; the stride of 20 puts
+// the 16 lanes of each dwordx4 read group on distinct 16-byte bank slots.
+constexpr uint32_t RING_STRIDE = 20;
 
 struct Ckpt {
     uint64_t* base;  // this block's sidecar entries, or nullptr
@@ -390,7 +396,6 @@ struct EncSmem {
     static constexpr uint32_t SIZE = 1u << LMAX;
     uint16_t st[BPW][SIZE];
     uint2 tt[BPW][256];
-    uint32_t hdrw[BPW][HDR_MAX / 4];
     // phase-1 scratch (statistics, header, spread) and phase-2 scratch
     // (trajectories, end states, merge list) share the same LDS: 13.4 KB per
     // workgroup at L <= 11, so 12 workgroups fit a CU (the VGPR limit)
@@ -398,6 +403,7 @@ struct EncSmem {
         struct {
             union {
                 uint32_t hs[HIST_WORDS];  // sub-histograms (counts[] go to cnt[], free until the spread)
+                uint32_t hdrw[HDR_MAX / 4];  // NCount header, stored to the slot before the spread
                 struct {
                     __attribute__((aligned(16))) uint8_t sym_at[SIZE];
                     __attribute__((aligned(16))) uint8_t occ_sym[SIZE];
@@ -410,8 +416,7 @@ struct EncSmem {
         struct {
             union {
                 uint2 cp[64 * TRACK_SLOTS];  // count-pass trajectories (Track)
-                uint32_t ring[64 * 36];   // emit: 32-word output ring per lane (stride 36: 16-byte
-                                          // aligned, conflict-free dwordx4 reads)
+                uint32_t ring[64 * RING_STRIDE];  // emit: 16-word output ring per lane (Emit)
             } u;
             uint32_t cntF[BPW][T + 1];
             uint32_t emF[BPW][T + 1];  // scratch path: end states of the emit pass
@@ -423,6 +428,7 @@ struct EncSmem {
     uint32_t info_new[BPW];  // block takes the scratch path
     uint32_t info_L[BPW];
     uint32_t info_hl[BPW];
+    uint32_t info_hv[BPW];  // the header's last partial word (merged with the payload's first bits)
     int scratch[4];
 };
 
@@ -473,9 +479,19 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
         if (lane == 0) sm.info_new[b] = newp ? 1u : 0u;
         FSE_STAMP(P, 2);
         if (rc == FSE_OK) {
-            const int hl = wave_header_write(sm.ph.p1.norm, L, tl, sm.hdrw[b]);
+            const int hl = wave_header_write(sm.ph.p1.norm, L, tl, sm.ph.p1.u.hdrw);
             if (lane == 0) sm.scratch[1] = hl;
-            if (hl < 0) rc = hl;
+            if (hl < 0) {
+                rc = hl;
+            } else {
+                // whole header words go to the slot now (no payload store
+                // touches them); the last partial word is merged at the end
+                const uint32_t* h = sm.ph.p1.u.hdrw;
+                uint32_t* gw = reinterpret_cast<uint32_t*>(P.out + gb * P.slot_bytes);
+                for (uint32_t w = lane; w < (uint32_t)hl / 4u; w += WAVE) gw[w] = h[w];
+                if (lane == 0) sm.info_hv[b] = (hl & 3) ? h[hl / 4] & ((1u << (8u * (hl & 3))) - 1u) : 0u;
+            }
+            wave_sync();  // the spread reuses the header's LDS
         }
         FSE_STAMP(P, 3);
         if (rc == FSE_OK) {
@@ -593,7 +609,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
         // the lane's whole stream (including the finals and marker of lane 0)
         // into its scratch words; checkpoints at lane-local bit positions
         auto emit_lane = [&]() -> uint32_t {
-            em.start(sw, 0, P.scr_lane_words, &sm.ph.p2.u.ring[lane * 36u]);
+            em.start(sw, 0, P.scr_lane_words, &sm.ph.p2.u.ring[lane * RING_STRIDE]);
             EncState e0;
             if (k == ktop) {
                 e0 = top_start<PASS_EMIT, NS>(blk, n, tab, em);
@@ -695,7 +711,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     __syncthreads();
     if (act && fits) {
         em.start(gw, off, (P.debug & 4u) ? 0u : (uint32_t)(P.slot_bytes >> 2),  // debug bit 2: no payload stores (ablation)
-                 &sm.ph.p2.u.ring[lane * 36u]);
+                 &sm.ph.p2.u.ring[lane * RING_STRIDE]);
         if (newp) {
             // the lane's stream at its final offset: whole words through the
             // emitter (ring, 64-byte groups, merge list), then the tail bits
@@ -791,18 +807,10 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
             sm.ph.p2.mval[b][slot + 1] = em.lo;
         }
     }
-    // header: whole words stored directly, the last partial word merged
-    if (live && fits) {
-        const uint8_t* h = reinterpret_cast<const uint8_t*>(sm.hdrw[b]);
-        for (uint32_t w = k; w < hl / 4u; w += T)
-            gw[w] = (uint32_t)h[4 * w] | ((uint32_t)h[4 * w + 1] << 8) | ((uint32_t)h[4 * w + 2] << 16) |
-                    ((uint32_t)h[4 * w + 3] << 24);
-        if (k == 0 && (hl & 3u)) {
-            uint32_t v = 0;
-            for (uint32_t i = hl & ~3u; i < hl; ++i) v |= (uint32_t)h[i] << (8u * (i & 3u));
-            sm.ph.p2.mword[b][0] = hl / 4u;
-            sm.ph.p2.mval[b][0] = v;
-        }
+    // header: whole words were stored in phase 1; the last partial word is merged
+    if (live && fits && k == 0 && (hl & 3u)) {
+        sm.ph.p2.mword[b][0] = hl / 4u;
+        sm.ph.p2.mval[b][0] = sm.info_hv[b];
     }
     FSE_STAMP(P, 7);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stores above land before the merge rewrites
@@ -2066,17 +2074,17 @@ hipError_t launch_encode(const EncParams& P, uint32_t lmax, hipStream_t stream) 
     const uint32_t bpw = 64u / T;
     const dim3 g((P.n_blocks + bpw - 1u) / bpw), b(64);
     if (P.nstates == 1) {  // fse_compress (lib.rs:112-143)
-        if (lmax <= 11) hipLaunchKernelGGL((encode_blocks_kernel<11, 64, 1>), g, b, 0, stream, P);
-        else hipLaunchKernelGGL((encode_blocks_kernel<12, 64, 1>), g, b, 0, stream, P);
+        if (lmax <= 11) hipLaunchKernelGGL((encode_blocks_kernel<11, 64, 1>), g, b, P.xlds, stream, P);
+        else hipLaunchKernelGGL((encode_blocks_kernel<12, 64, 1>), g, b, P.xlds, stream, P);
     } else if (T == 64 && P.scratch) {  // scratch path built in (FSEHIP_ENC_PATH=0|2)
-        if (lmax <= 11) hipLaunchKernelGGL((encode_blocks_kernel<11, 64, 2, true>), g, b, 0, stream, P);
-        else hipLaunchKernelGGL((encode_blocks_kernel<12, 64, 2, true>), g, b, 0, stream, P);
+        if (lmax <= 11) hipLaunchKernelGGL((encode_blocks_kernel<11, 64, 2, true>), g, b, P.xlds, stream, P);
+        else hipLaunchKernelGGL((encode_blocks_kernel<12, 64, 2, true>), g, b, P.xlds, stream, P);
     } else if (T == 64) {
-        if (lmax <= 11) hipLaunchKernelGGL((encode_blocks_kernel<11, 64, 2>), g, b, 0, stream, P);
-        else hipLaunchKernelGGL((encode_blocks_kernel<12, 64, 2>), g, b, 0, stream, P);
+        if (lmax <= 11) hipLaunchKernelGGL((encode_blocks_kernel<11, 64, 2>), g, b, P.xlds, stream, P);
+        else hipLaunchKernelGGL((encode_blocks_kernel<12, 64, 2>), g, b, P.xlds, stream, P);
     } else {
-        if (lmax <= 11) hipLaunchKernelGGL((encode_blocks_kernel<11, 32, 2>), g, b, 0, stream, P);
-        else hipLaunchKernelGGL((encode_blocks_kernel<12, 32, 2>), g, b, 0, stream, P);
+        if (lmax <= 11) hipLaunchKernelGGL((encode_blocks_kernel<11, 32, 2>), g, b, P.xlds, stream, P);
+        else hipLaunchKernelGGL((encode_blocks_kernel<12, 32, 2>), g, b, P.xlds, stream, P);
     }
     return hipGetLastError();
 }
