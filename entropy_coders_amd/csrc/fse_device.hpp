@@ -31,45 +31,56 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
-// Inclusive prefix sum across the wave (6 DPP-able shuffle steps).
+// Inclusive scans across the wave on DPP (VALU lane moves, a few cycles
+// each) instead of ds_bpermute shuffles (an LDS round trip each): row_shr
+// 1/2/4/8 within each 16-lane row, then row_bcast:15 and row_bcast:31 carry
+// the row totals (GFX9 DPP).  Identity 0 (unsigned sum and max); out-of-row
+// sources and masked rows read 0.  Call with every lane of the wave active.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp0(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xf, true);
+}
+template <class Op>
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, Op op) {
+    v = op(v, dpp0<0x111, 0xf>(v));  // row_shr:1
+    v = op(v, dpp0<0x112, 0xf>(v));  // row_shr:2
+    v = op(v, dpp0<0x114, 0xf>(v));  // row_shr:4
+    v = op(v, dpp0<0x118, 0xf>(v));  // row_shr:8
+    v = op(v, dpp0<0x142, 0xa>(v));  // row_bcast:15 into rows 1 and 3
+    v = op(v, dpp0<0x143, 0xc>(v));  // row_bcast:31 into rows 2 and 3
+    return v;
+}
 __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        uint32_t o = __shfl_up(v, d, 64);
-        if ((int)lane_id() >= d) v += o;
-    }
-    return v;
-}
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-    return v;
-}
-__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v = max(v, (uint32_t)__shfl_xor(v, d, 64));
-    return v;
+    return wave_incl_scan(v, [](uint32_t a, uint32_t b) { return a + b; });
 }
 __device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        uint32_t o = __shfl_up(v, d, 64);
-        if ((int)lane_id() >= d) v = max(v, o);
-    }
-    return v;
+    return wave_incl_scan(v, [](uint32_t a, uint32_t b) { return max(a, b); });
+}
+// Lane 63's value on the scalar unit (wave-uniform).
+__device__ __forceinline__ uint32_t bcast63(uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)v, 63); }
+// Reductions: the scan's last lane, read on the scalar unit (wave-uniform).
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum(v), 63);
+}
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max(v), 63);
 }
 
-// Lanes of the wave holding the same 8-bit key (8 ballots), restricted to
-// the active lanes.
-__device__ __forceinline__ uint64_t match_u8(uint32_t key, uint64_t active) {
+// Lanes of the wave holding the same key (one ballot per key bit),
+// restricted to the active lanes.  Keys are symbols < table_len, so only
+// kbits = bits of (table_len - 1) need comparing (wave-uniform; 6 for C2's
+// 48 symbols instead of 8).
+__device__ __forceinline__ uint64_t match_key(uint32_t key, uint64_t active, uint32_t kbits) {
     uint64_t peers = active;
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
+    for (uint32_t b = 0; b < 8; ++b) {
+        if (b >= kbits) break;
         uint64_t bal = __ballot((key >> b) & 1u);
         peers &= ((key >> b) & 1u) ? bal : ~bal;
     }
     return peers;
 }
+__device__ __forceinline__ uint32_t key_bits(uint32_t tl) { return tl <= 1u ? 1u : 32u - (uint32_t)__clz(tl - 1u); }
 
 // ---------------------------------------------------------------------------
 // Histogram::new (histogram.rs:18-66): 256-bin count of one block by one
@@ -456,7 +467,7 @@ __device__ inline int wave_header_write(const int32_t* norm, uint32_t L, uint32_
         }
     }
     const uint32_t ex_bits = wave_incl_sum(nbits) - nbits;
-    const uint32_t total = 4u + __shfl(ex_bits + nbits, 63, 64);
+    const uint32_t total = 4u + bcast63(ex_bits + nbits);
     const uint32_t bytes = (total + 7u) >> 3;
     if (bytes > HDR_MAX) return FSE_ERR_DST_TOO_SMALL;
     wave_sync();
@@ -730,8 +741,8 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
     const uint32_t ex_c = wave_incl_sum(sum_c) - sum_c;
     const uint32_t ex_p = wave_incl_sum(sum_p) - sum_p;
     const uint32_t ex_n = wave_incl_sum(sum_neg) - sum_neg;
-    const uint32_t total_neg = __shfl(ex_n + sum_neg, 63, 64);
-    const uint32_t total_pos = __shfl(ex_p + sum_p, 63, 64);
+    const uint32_t total_neg = bcast63(ex_n + sum_neg);
+    const uint32_t total_pos = bcast63(ex_p + sum_p);
     if (total_pos + total_neg > size || total_neg > size) return FSE_ERR_BAD_TABLE;
     const int32_t ht = (int32_t)size - 1 - (int32_t)total_neg;
     for (uint32_t i = lane; i < size / 16u; i += WAVE) {  // size >= 32: whole 16-byte stores
@@ -762,7 +773,7 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
             uint32_t v = (j < total_pos) ? occ_sym[j] : 0u;
             uint32_t f = max(wave_incl_max(v), carry);
             if (j < total_pos) occ_sym[j] = (uint8_t)f;
-            carry = __shfl(f, 63, 64);
+            carry = bcast63(f);
         }
     }
     wave_sync();
@@ -789,7 +800,7 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
         bool act = i < size;
         uint64_t active = __ballot(act);
         uint32_t s = act ? sym_at[i] : 0u;
-        uint64_t peers = match_u8(s, active);
+        uint64_t peers = match_key(s, active, key_bits(tl));
         uint32_t before = act ? cnt[s] : 0u;
         uint32_t r = before + (uint32_t)__popcll(peers & lanemask_lt());
         wave_sync();
@@ -838,8 +849,8 @@ __device__ inline int block_build_spread(const int32_t* norm, uint32_t L, uint32
         const uint32_t ex_c = wave_incl_sum(sum_c) - sum_c;
         const uint32_t ex_p = wave_incl_sum(sum_p) - sum_p;
         const uint32_t ex_n = wave_incl_sum(sum_neg) - sum_neg;
-        const uint32_t total_neg = __shfl(ex_n + sum_neg, 63, 64);
-        const uint32_t total_pos = __shfl(ex_p + sum_p, 63, 64);
+        const uint32_t total_neg = bcast63(ex_n + sum_neg);
+        const uint32_t total_pos = bcast63(ex_p + sum_p);
         const bool ok = total_pos + total_neg <= size;
         uint32_t c = ex_c, p = ex_p, ng = ex_n;
 #pragma unroll
@@ -872,7 +883,7 @@ __device__ inline int block_build_spread(const int32_t* norm, uint32_t L, uint32
             const uint32_t v = (j < o1) ? occ_sym[j] : 0u;
             const uint32_t f = max(wave_incl_max(v), carry);
             if (j < o1) occ_sym[j] = (uint8_t)f;
-            carry = __shfl(f, 63, 64);
+            carry = bcast63(f);
         }
         if (lane == 0) wscr[wv] = carry;
     }
@@ -930,7 +941,7 @@ __device__ inline int block_build_spread(const int32_t* norm, uint32_t L, uint32
             const bool act = i < i1;
             const uint64_t active = __ballot(act);
             const uint32_t s = act ? sym_at[i] : 0u;
-            const uint64_t peers = match_u8(s, active);
+            const uint64_t peers = match_key(s, active, key_bits(tl));
             const uint32_t before = act ? mycnt[s] : 0u;
             const uint32_t rk = before + (uint32_t)__popcll(peers & lanemask_lt());
             wave_sync();

@@ -22,7 +22,8 @@ struct EncParams {
     int32_t* status;
     uint32_t lanes;  // encoder lanes per block (32 or 64; 0 = default)
     uint32_t nstates;  // 2 = fse_compress2 (default), 1 = fse_compress
-    uint32_t debug;  // ablation: bit0 = tables only, bit1 = no emit pass, bit2 = no payload stores
+    uint32_t debug;  // ablation: bit0 = tables only, bit1 = no emit pass, bit2 = no payload stores,
+                     // bit3 = histogram only, bit4 = no repair rounds
     uint64_t* stamps;  // diagnostics: per-workgroup s_memtime at phase ends
     // Scratch-emit path (see encode_blocks_kernel): each lane writes its
     // bits to a lane-private scratch stream from the start state the count

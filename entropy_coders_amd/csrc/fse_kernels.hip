@@ -45,13 +45,23 @@ __device__ __forceinline__ uint4 load_chunk(const uint8_t* blk, uint32_t n, uint
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-// Encoder tables in LDS: stateTable as bytes and the symbol transforms
-// {deltaNbBits, byte offset of stateTable[deltaFindState]} (fse.rs:165-188),
-// so one state step is add, shift, shift-add, ds_read_u16.
+// Encoder tables in LDS: stateTable (u16 entries, fse.rs:157-162) and the
+// symbol transforms {deltaNbBits, LDS byte address of
+// stateTable[deltaFindState]} (fse.rs:165-188): the block's table base is
+// folded into the transform, so one state step is add, shift, shift-add,
+// ds_read_u16 whichever table of the workgroup the lane uses.
 struct EncTab {
-    const uint8_t* st;  // stateTable, u16 entries (fse.rs:157-162)
-    const uint2* tt;    // {deltaNbBits, 2 * deltaFindState}
+    const uint2* tt;  // {deltaNbBits, LDS address of stateTable + 2 * deltaFindState}
 };
+typedef __attribute__((address_space(3))) const uint16_t lds_cu16;
+__device__ __forceinline__ uint32_t st_at(uint32_t lds_addr) {
+    return *(lds_cu16*)(uintptr_t)lds_addr;
+}
+// LDS byte address of a __shared__ object
+template <class P>
+__device__ __forceinline__ uint32_t lds_addr_of(P* p) {
+    return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) P*)p;
+}
 
 // Bit emitter into a 32-bit-word view of the output slot.  Bits are
 // appended LSB-first (writer.rs:140-180); every completed word is stored,
@@ -206,7 +216,7 @@ struct EncState {
 __device__ __forceinline__ uint32_t enc_step(uint32_t& x, uint32_t s, const EncTab& T) {
     const uint2 t = T.tt[s];
     const uint32_t nb = (t.x + x) >> 16;
-    x = *reinterpret_cast<const uint16_t*>(T.st + ((x >> nb) << 1) + (int32_t)t.y);
+    x = st_at(((x >> nb) << 1) + t.y);
     return nb;
 }
 
@@ -234,7 +244,7 @@ __device__ __forceinline__ void enc_chunk(const uint4& q, uint32_t c8, uint32_t 
             const uint2 t = (j & 1) ? t1[j >> 1] : t0[j >> 1];
             const uint32_t v0 = x0;
             const uint32_t nb0 = (t.x + x0) >> 16;
-            x0 = *reinterpret_cast<const uint16_t*>(T.st + ((x0 >> nb0) << 1) + (int32_t)t.y);
+            x0 = st_at(((x0 >> nb0) << 1) + t.y);
             if (MODE == PASS_COUNT || MODE == PASS_REPAIR) bits += nb0;
             if (MODE == PASS_EMIT) {
                 em.put(__builtin_amdgcn_ubfe(v0, 0u, nb0), nb0);
@@ -249,9 +259,9 @@ __device__ __forceinline__ void enc_chunk(const uint4& q, uint32_t c8, uint32_t 
         if (!FULL && c8 + (uint32_t)j >= pb) continue;
         const uint32_t v1 = x1, v0 = x0;
         const uint32_t nb1 = (t1[j].x + x1) >> 16;
-        x1 = *reinterpret_cast<const uint16_t*>(T.st + ((x1 >> nb1) << 1) + (int32_t)t1[j].y);
+        x1 = st_at(((x1 >> nb1) << 1) + t1[j].y);
         const uint32_t nb0 = (t0[j].x + x0) >> 16;
-        x0 = *reinterpret_cast<const uint16_t*>(T.st + ((x0 >> nb0) << 1) + (int32_t)t0[j].y);
+        x0 = st_at(((x0 >> nb0) << 1) + t0[j].y);
         if (MODE == PASS_COUNT || MODE == PASS_REPAIR) bits += nb1 + nb0;
         if (MODE == PASS_EMIT) {
             const uint32_t pairbits = (__builtin_amdgcn_ubfe(v0, 0u, nb0) << nb1) | __builtin_amdgcn_ubfe(v1, 0u, nb1);
@@ -354,7 +364,7 @@ __device__ __forceinline__ uint32_t enc_init(const EncTab& T, uint32_t s) {
     const uint2 t = T.tt[s];
     const uint32_t bo = (t.x + (1u << 15)) >> 16;
     const uint32_t v = (bo << 16) - t.x;
-    return *reinterpret_cast<const uint16_t*>(T.st + ((v >> bo) << 1) + (int32_t)t.y);
+    return st_at(((v >> bo) << 1) + t.y);
 }
 
 // Exact state of the topmost lane before the main loop.  NS = 2: both
@@ -502,21 +512,23 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
                                    [&](uint32_t i, uint32_t s, uint32_t r) {
                                        st[cumul[s] + r] = (uint16_t)(size + i);  // fse.rs:157-162
                                    });
-            // symbol transforms, fse.rs:165-188 (total == cumul[s])
+            // symbol transforms, fse.rs:165-188 (total == cumul[s]), with
+            // the stateTable's LDS address folded into deltaFindState
+            const uint32_t stb = lds_addr_of(&sm.st[b][0]);
             for (uint32_t s = lane; s < 256; s += WAVE) {
                 int32_t x = (s < tl) ? sm.ph.p1.norm[s] : 0;
-                uint2 t = make_uint2(0, 0);
+                uint2 t = make_uint2(0, stb);
                 if (s < tl) {
                     const int32_t tot = (int32_t)sm.ph.p1.cumul[s];
                     if (x == 0) {
                         t.x = ((L + 1u) << 16) - (1u << L);
                     } else if (x == -1 || x == 1) {
                         t.x = (L << 16) - (1u << L);
-                        t.y = (uint32_t)(2 * (tot - 1));
+                        t.y = stb + (uint32_t)(2 * (tot - 1));
                     } else {
                         const uint32_t mb = L - ilog2u((uint32_t)(x - 1));
                         t.x = (mb << 16) - ((uint32_t)x << mb);
-                        t.y = (uint32_t)(2 * (tot - x));
+                        t.y = stb + (uint32_t)(2 * (tot - x));
                     }
                 }
                 sm.tt[b][s] = t;
@@ -546,7 +558,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     const uint32_t n = live ? (uint32_t)min((uint64_t)P.block_size, P.n_total - boff) : 0u;
     const uint8_t* blk = P.src + boff;
     const uint32_t L = sm.info_L[b];
-    const EncTab tab{reinterpret_cast<const uint8_t*>(sm.st[b]), sm.tt[b]};
+    const EncTab tab{sm.tt[b]};
     // main-loop steps: pairs (NS = 2) or symbols below the seed (NS = 1)
     const uint32_t Pm = live ? (NS == 2 ? ((n & 1u) ? (n - 3u) / 2u : n / 2u - 1u) : n - 1u) : 0u;
     constexpr uint32_t SPC = NS == 2 ? 8u : 16u;  // steps per 16-byte chunk
@@ -662,6 +674,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
         }
         FSE_STAMP(P, 5);
         for (;;) {
+            if (P.debug & 16u) break;  // ablation: no repair (wrong output)
             __syncthreads();
             bool bad = false;
             uint32_t nbF = 0;
@@ -1665,7 +1678,7 @@ __global__ __launch_bounds__(64 * NW) void decode_pre_kernel(DecParams P) {
         // VAR 6: lane t decodes segment 33t mod NT of each round, so lanes
         // that walk their segments in lockstep read words ~33 segments apart
         // (spread over the banks) instead of ~1 segment (~32 words) apart
-        const uint32_t seg = base + (VAR == 6 ? ((tid * 33u) & (NT - 1u)) : tid);
+        const uint32_t seg = base + ((VAR == 6 || VAR == 0 || VAR == 1) ? ((tid * 33u) & (NT - 1u)) : tid);
         if (seg >= nseg) continue;
         const uint64_t e = sc[seg];
         const uint32_t p0 = seg * I, p1 = min(p0 + I, Pm);
@@ -2139,6 +2152,8 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
                 } else if (P.variant == 3) go(decode_pre_kernel<11, 4, PP, 3>, 256);
                 else if (P.variant == 5) go(decode_pre_kernel<11, 4, PP, 5>, 256);
                 else if (P.variant == 6) go(decode_pre_kernel<11, 4, PP, 6>, 256);
+                else if (P.variant == 10) go(decode_pre_kernel<11, 4, PP, 0>, 256);
+                else if (P.variant == 11) go(decode_pre_kernel<11, 4, PP, 1>, 256);
                 else if (P.stage_kib == 40) go(decode_pre_kernel<11, 4, (40u << 10), 2>, 256);
                 else if (P.stage_kib == 36) go(decode_pre_kernel<11, 4, (36u << 10), 2>, 256);
                 else {

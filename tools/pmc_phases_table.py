@@ -6,7 +6,7 @@ import sys
 d = sys.argv[1]
 for D in ("8", "1", "2", "4", "0"):
     vals = {}
-    for f in glob.glob(f"{d}/d{D}/**/*counter_collection.csv", recursive=True):
+    for f in glob.glob(f"{d}/{D}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
             if "encode_blocks" in r["Kernel_Name"]:
                 vals[r["Counter_Name"]] = float(r["Counter_Value"])
