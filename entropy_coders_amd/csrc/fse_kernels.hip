@@ -1834,7 +1834,7 @@ __global__ __launch_bounds__(64) void decode1_serial_kernel(DecParams P) {
 // stream, e.g. from the CPU crate), optionally recording the sidecar.
 // The two interleaved decoders make the stream essentially serial: a
 // decoder started mid-block with guessed states practically never falls
-// into step with the exact one (tools/syncsim.py: 35 of 40 random starts in
+// into step with the exact one (oracle/syncsim.py: 35 of 40 random starts in
 // a C2 block never did, the rest after 25K-40K symbols), so speculative
 // segment decoding cannot replace the sidecar for this
 // format.  The serial decode is instead made as short a dependency chain
@@ -2153,7 +2153,8 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
                 if (P.variant == 3) go(decode_pre_kernel<11, 8, PP, 3>, 512);
                 else if (P.variant == 5) go(decode_pre_kernel<11, 8, PP, 5>, 512);
                 else if (P.variant == 6) go(decode_pre_kernel<11, 8, PP, 6>, 512);
-                else go(decode_pre_kernel<11, 8, PP, 2>, 512);
+                else if (P.variant == 2) go(decode_pre_kernel<11, 8, PP, 2>, 512);
+                else go(decode_pre_kernel<11, 8, PP, 9>, 512);
             } else {
                 if (P.variant == 3) go(decode_pre_kernel<12, 8, PP - 8192, 3>, 512);
                 else if (P.variant == 5) go(decode_pre_kernel<12, 8, PP - 8192, 5>, 512);
