@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-c3", action="store_true", help="skip the decode-only (prebuilt tables) line")
+    ap.add_argument("--no-sweep", action="store_true", help="skip the C5 distribution / table-log sweep")
+    ap.add_argument("--sweep-bytes", type=int, default=256 << 20, help="raw bytes per C5 sweep point")
     ap.add_argument("--host", action="store_true",
                     help="also time the host-streaming pipeline (pinned host buffers, PCIe copies overlapped "
                          "with the kernels); reported separately, never in value")
@@ -119,6 +121,53 @@ def cpu_baseline(src_host: np.ndarray, block: int, budget_s: float) -> dict:
         "single_core_32KiB_lut0.2": {"encode_MiB_s": round(enc1 / 2**20, 1),
                                      "decode_MiB_s": round(dec1 / 2**20, 1)},
     }
+
+
+C5_SWEEP = [  # BASELINE.json configs[4]: (name, generator kind, LUT p, table log)
+    *[("near-uniform (0..239, H~7.9 bits)", 2, 0.0, L) for L in (9, 10, 11, 12)],
+    *[("skewed (LUT p=0.77, H~1.0 bit)", 0, 0.77, L) for L in (9, 10, 11, 12)],
+    ("LUT p=0.05 (normalize_slow path)", 0, 0.05, 9),
+]
+
+
+def c5_sweep(dev, nbytes: int, block: int, ckpt: int, reps: int = 3) -> list:
+    """C5 distribution sweep on one GPU, after the timed step: encode and
+    decode of `nbytes` per distribution and explicit table log (histogram.rs:95
+    normalize(L)), HIP-event timed, round trip verified.  Reported beside the
+    bench line, never in `value`."""
+    import torch
+
+    from entropy_coders_amd import BlockCodec
+
+    stream = torch.cuda.current_stream(dev)
+    rows = []
+    for name, kind, prob, L in C5_SWEEP:
+        codec = BlockCodec(block_size=block, table_log=L, ckpt_interval=ckpt, device=dev)
+        src = codec.generate(kind, prob, 0x5EED0005, nbytes)
+        cb = codec.alloc(nbytes)
+        out = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        st = torch.zeros(codec.n_blocks(nbytes), dtype=torch.int32, device=dev)
+        codec.compress_into(src, cb)
+        codec.decompress_into(cb, out, st)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        ev[0].record(stream)
+        for _ in range(reps):
+            codec.compress_into(src, cb)
+        ev[1].record(stream)
+        for _ in range(reps):
+            codec.decompress_into(cb, out, st)
+        ev[2].record(stream)
+        torch.cuda.synchronize(dev)
+        enc_ms = ev[0].elapsed_time(ev[1]) / reps
+        dec_ms = ev[1].elapsed_time(ev[2]) / reps
+        ok = (int(cb["status"].abs().max()) == 0 and int(st.abs().max()) == 0 and bool(torch.equal(out, src)))
+        comp = int(cb["comp_len"].to(torch.int64).sum())
+        rows.append({"dist": name, "table_log": L, "compressed_ratio": round(comp / nbytes, 4),
+                     "encode_GiB_s": round(nbytes / (enc_ms * 1e-3) / 2**30, 1),
+                     "decode_GiB_s": round(nbytes / (dec_ms * 1e-3) / 2**30, 1),
+                     "roundtrip_GiB_s": round(nbytes / ((enc_ms + dec_ms) * 1e-3) / 2**30, 1), "verified": ok})
+        del codec, src, cb, out, st
+    return rows
 
 
 def main():
@@ -333,6 +382,12 @@ def main():
             line["gather"] = gather_info
         if host_info is not None:
             line["host_pipeline"] = host_info
+        if not args.no_sweep and args.nstates == 2:
+            sw = c5_sweep(dev, args.sweep_bytes, args.block, args.ckpt)
+            line["c5_sweep"] = {"workload": f"C5: {args.sweep_bytes >> 20} MiB per distribution and table log, "
+                                            "encode + decode (2-state), 1 GPU", "rows": sw}
+            ok = ok and all(r["verified"] for r in sw)
+            line["verified_roundtrip"] = ok
         if world == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(src.cpu().numpy(), args.block, args.cpu_seconds)
         print(json.dumps(line), flush=True)
