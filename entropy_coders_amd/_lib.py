@@ -10,7 +10,9 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libfsehip.so")
+# FSEHIP_LIB: an alternative in-tree build of the same library (A/B timing
+# of compile-time variants, e.g. libfsehip_alt.so); the product is libfsehip.so.
+LIB_PATH = os.path.join(HERE, os.environ.get("FSEHIP_LIB", "libfsehip.so"))
 
 # every symbol include/fsehip.h declares (checked by tests/test_abi.py)
 EXPORTS = (

@@ -100,7 +100,11 @@ __device__ __forceinline__ uint32_t key_bits(uint32_t tl) { return tl <= 1u ? 1u
 // must not alias hs.
 // ---------------------------------------------------------------------------
 constexpr uint32_t HSUB = 8;
-constexpr uint32_t HIST_WORDS = 256 * HSUB / 2;
+#ifndef FSE_HIST_U16
+#define FSE_HIST_U16 1
+#endif
+constexpr bool HIST_U16 = FSE_HIST_U16 != 0;
+constexpr uint32_t HIST_WORDS = HIST_U16 ? 256 * HSUB / 2 : 256 * HSUB;
 constexpr uint32_t HIST_SEG = 1u << 18;
 
 // The counting loop is a call of its own (noinline): inlined, it raised the
@@ -116,11 +120,11 @@ __device__ __attribute__((noinline)) void wave_histogram_seg(const uint8_t* __re
                                                              uint32_t* hs_generic) {
     const uint32_t lane = lane_id();
     // byte address of this lane's copy: ((lane / 2) % 4) words into each bin's 4
-    lds_u32* mine = (lds_u32*)hs_generic + ((lane >> 1) & 3u);
-    const uint32_t inc = 1u << (16u * (lane & 1u));
+    lds_u32* mine = (lds_u32*)hs_generic + (HIST_U16 ? ((lane >> 1) & 3u) : (lane & 7u));
+    const uint32_t inc = HIST_U16 ? 1u << (16u * (lane & 1u)) : 1u;
     gbl_u8* src = (gbl_u8*)src_generic;
     auto add = [&](uint32_t byte) {
-        __hip_atomic_fetch_add(&mine[byte * 4u], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(&mine[byte * (HIST_WORDS / 256u)], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
     uint32_t done = 0;
     if ((reinterpret_cast<uintptr_t>(src_generic) & 15u) == 0) {
@@ -182,9 +186,14 @@ __device__ inline uint32_t wave_histogram(const uint8_t* __restrict__ src, uint3
         wave_histogram_seg(src + seg, m, hs);
         wave_sync();
         for (uint32_t s = lane; s < 256; s += WAVE) {
-            const uint4 q = reinterpret_cast<const uint4*>(hs)[s];
-            counts[s] += (q.x & 0xFFFFu) + (q.x >> 16) + (q.y & 0xFFFFu) + (q.y >> 16) + (q.z & 0xFFFFu) +
-                         (q.z >> 16) + (q.w & 0xFFFFu) + (q.w >> 16);
+            if (HIST_U16) {
+                const uint4 q = reinterpret_cast<const uint4*>(hs)[s];
+                counts[s] += (q.x & 0xFFFFu) + (q.x >> 16) + (q.y & 0xFFFFu) + (q.y >> 16) + (q.z & 0xFFFFu) +
+                             (q.z >> 16) + (q.w & 0xFFFFu) + (q.w >> 16);
+            } else {
+                const uint4 q = reinterpret_cast<const uint4*>(hs)[2 * s], r = reinterpret_cast<const uint4*>(hs)[2 * s + 1];
+                counts[s] += q.x + q.y + q.z + q.w + r.x + r.y + r.z + r.w;
+            }
         }
         wave_sync();
         seg += m;
