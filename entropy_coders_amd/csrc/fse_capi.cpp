@@ -347,7 +347,7 @@ static int decompress_impl(const fsehip_params* p, const uint8_t* d_in, uint64_t
     P.sidecar_out = d_sidecar_out;
     P.debug = env_u32("FSEHIP_DEBUG", 0) >> 4;
     P.waves = env_u32("FSEHIP_DEC_WAVES", 4) == 8 ? 8 : 4;
-    P.variant = env_u32("FSEHIP_DEC_VAR", 9);
+    P.variant = env_u32("FSEHIP_DEC_VAR", 12);
     P.dual = env_u32("FSEHIP_DEC_DUAL", 0);
     P.stage_kib = env_u32("FSEHIP_DEC_PP", 44);
     // the decoder reads L from each header; size its tables for the bound

@@ -1017,7 +1017,10 @@ __device__ __forceinline__ uint32_t lds_bits(const uint32_t* pay, int32_t pos) {
 //   VAR 0: one ds_read2 of the two words at pos per pair;
 //   VAR 1: the same window fetched from pos_prev - 24 alongside the table
 //          reads (one LDS latency on the chain instead of two);
-//   VAR 9 (default in decode_pre_kernel): VAR 1 without the clamp (the image
+//   VAR 12 (default in decode_pre_kernel): VAR 9 reading one payload dword
+//          per pair (the upper word of the window is one of the previous
+//          pair's two words): C3 0.64 -> 0.60 ms.
+//   VAR 9: VAR 1 without the clamp (the image
 //          has a pad below it), with segments permuted over the lanes (lane
 //          t takes segment 33t mod NT) so that lockstep reads spread over the
 //          banks: branch-free, ~13 VALU + 3 LDS reads per pair (VAR 2: ~23
@@ -1044,6 +1047,10 @@ struct LdsChain {
             wlo = pay[k];
             whi = pay[k + 1];
             wnx = pay[max(k - 1, 0)];
+        }
+        if (VAR == 12) {  // the first pair reads word lo/32 and takes word lo/32 + 1 from here
+            B = (p - 24) & ~31;
+            whi = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(pay) + (B >> 3) + 4);
         }
     }
     __device__ __forceinline__ uint32_t pair(const uint32_t* pay, const uint8_t* dtb) {
@@ -1086,6 +1093,21 @@ struct LdsChain {
             e1 = *reinterpret_cast<const uint32_t*>(dtb + a1);
             pos -= (int32_t)((e0 + e1) & 0xFFu);
             x = (uint32_t)((((uint64_t)w1 << 32) | w0) >> ((uint32_t)pos - base));
+        } else if (VAR == 12) {
+            // VAR 9 with one payload dword per pair instead of two: a pair
+            // consumes <= 24 < 32 bits, so the window base lo moves down by at
+            // most one word per pair and the upper word is always one of the
+            // previous pair's two words (B = previous lo)
+            const int32_t lo = (pos - 24) & ~31;
+            const uint32_t w0 = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(pay) + (lo >> 3));
+            e0 = *reinterpret_cast<const uint32_t*>(dtb + a0);
+            e1 = *reinterpret_cast<const uint32_t*>(dtb + a1);
+            const uint32_t w1 = lo == B ? whi : wlo;
+            pos -= (int32_t)((e0 + e1) & 0xFFu);
+            x = (uint32_t)((((uint64_t)w1 << 32) | w0) >> (uint32_t)(pos - lo));
+            B = lo;
+            whi = w1;
+            wlo = w0;
         } else if (VAR == 9) {
             // VAR 1 without the clamp: the decode_pre_kernel image has a
             // 16-byte pad below it, so the window may start at word -1
@@ -1694,7 +1716,7 @@ __global__ __launch_bounds__(64 * NW) void decode_pre_kernel(DecParams P) {
         // VAR 6: lane t decodes segment 33t mod NT of each round, so lanes
         // that walk their segments in lockstep read words ~33 segments apart
         // (spread over the banks) instead of ~1 segment (~32 words) apart
-        const uint32_t seg = base + ((VAR == 6 || VAR == 0 || VAR == 1 || VAR == 9) ? ((tid * 33u) & (NT - 1u)) : tid);
+        const uint32_t seg = base + ((VAR == 6 || VAR == 0 || VAR == 1 || VAR == 9 || VAR == 12) ? ((tid * 33u) & (NT - 1u)) : tid);
         if (seg >= nseg) continue;
         const uint64_t e = sc[seg];
         const uint32_t p0 = seg * I, p1 = min(p0 + I, Pm);
@@ -2154,7 +2176,7 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
                 else if (P.variant == 5) go(decode_pre_kernel<11, 8, PP, 5>, 512);
                 else if (P.variant == 6) go(decode_pre_kernel<11, 8, PP, 6>, 512);
                 else if (P.variant == 2) go(decode_pre_kernel<11, 8, PP, 2>, 512);
-                else go(decode_pre_kernel<11, 8, PP, 9>, 512);
+                else go(decode_pre_kernel<11, 8, PP, 12>, 512);
             } else {
                 if (P.variant == 3) go(decode_pre_kernel<12, 8, PP - 8192, 3>, 512);
                 else if (P.variant == 5) go(decode_pre_kernel<12, 8, PP - 8192, 5>, 512);
@@ -2172,6 +2194,7 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
                 else if (P.variant == 10) go(decode_pre_kernel<11, 4, PP, 0>, 256);
                 else if (P.variant == 11) go(decode_pre_kernel<11, 4, PP, 1>, 256);
                 else if (P.variant == 2) go(decode_pre_kernel<11, 4, PP, 2>, 256);
+                else if (P.variant == 9) go(decode_pre_kernel<11, 4, PP, 9>, 256);
                 else if (P.stage_kib == 40) go(decode_pre_kernel<11, 4, (40u << 10), 2>, 256);
                 else if (P.stage_kib == 36) go(decode_pre_kernel<11, 4, (36u << 10), 2>, 256);
                 else {
@@ -2181,8 +2204,8 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
                     DecParams P1 = P, P2 = P;
                     P1.pass = 1;
                     P2.pass = 2;
-                    hipLaunchKernelGGL((decode_pre_kernel<11, 4, PP, 9>), g, dim3(256), 0, stream, P1);
-                    hipLaunchKernelGGL((decode_pre_kernel<11, 4, (66u << 10), 9>), g, dim3(256), 0, stream, P2);
+                    hipLaunchKernelGGL((decode_pre_kernel<11, 4, PP, 12>), g, dim3(256), 0, stream, P1);
+                    hipLaunchKernelGGL((decode_pre_kernel<11, 4, (66u << 10), 12>), g, dim3(256), 0, stream, P2);
                 }
             } else {
                 if (P.variant == 3) go(decode_pre_kernel<12, 4, PP - 8192, 3>, 256);
@@ -2191,8 +2214,8 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
                     DecParams P1 = P, P2 = P;
                     P1.pass = 1;
                     P2.pass = 2;
-                    hipLaunchKernelGGL((decode_pre_kernel<12, 4, PP - 8192, 9>), g, dim3(256), 0, stream, P1);
-                    hipLaunchKernelGGL((decode_pre_kernel<12, 4, (66u << 10), 9>), g, dim3(256), 0, stream, P2);
+                    hipLaunchKernelGGL((decode_pre_kernel<12, 4, PP - 8192, 12>), g, dim3(256), 0, stream, P1);
+                    hipLaunchKernelGGL((decode_pre_kernel<12, 4, (66u << 10), 12>), g, dim3(256), 0, stream, P2);
                 }
             }
         }
