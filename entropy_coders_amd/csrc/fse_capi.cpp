@@ -372,6 +372,7 @@ int fsehip_build_dtables(const fsehip_params* p, const uint8_t* d_in, uint64_t s
     if (n_blocks == 0) return FSE_OK;
     if (!device_ok()) return FSE_ERR_NO_DEVICE;
     fsehip::DtParams D{};
+    D.debug = env_u32("FSEHIP_DT_DEBUG", 0);
     D.in = d_in;
     D.slot_bytes = slot_bytes;
     D.comp_len = d_comp_len;

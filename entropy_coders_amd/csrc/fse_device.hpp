@@ -724,12 +724,21 @@ __device__ inline int header_read_wave(uint32_t r0, uint32_t r1, uint32_t n, uin
 // visited iff it is <= the high threshold, and the j-th visited position
 // gets the j-th positive occurrence in symbol order (fse.rs:139-150).  The
 // owner of occurrence j comes from a forward max-fill of symbol start marks.
-// Ranks come from 8-ballot peer matching over 64 consecutive positions plus
-// running per-symbol counters.
+// Both walks take 4 consecutive entries per lane, so a 2^11 table needs 8
+// wave steps per walk instead of 32.
+// Ranks come from ballot peer matching over 64 consecutive positions.  With
+// RK (LDS, 2 x 2^L bytes) and table_len <= 64 they take two passes without
+// a serial chain: per-chunk symbol counts, a per-symbol prefix over chunks,
+// then rank = prefix + peers below; otherwise running per-symbol counters
+// (an LDS read-modify-write per chunk).
 // ---------------------------------------------------------------------------
-template <typename Visit>
+// Exclusive scan helpers on DPP: wave_shr:1 (lane 0 reads 0).
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v) { return dpp0<0x138, 0xf>(v); }
+
+template <uint32_t MAXCH = 64, typename Visit>  // MAXCH: 2^LMAX / 64 chunks (two-pass ranks)
 __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_t tl, uint8_t* sym_at,
-                                        uint8_t* occ_sym, uint16_t* cumul, uint32_t* cnt, Visit visit) {
+                                        uint8_t* occ_sym, uint16_t* cumul, uint32_t* cnt, Visit visit,
+                                        uint16_t* RK = nullptr) {
     const uint32_t lane = lane_id();
     const uint32_t size = 1u << L;
     const uint32_t mask = size - 1u;
@@ -774,35 +783,94 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
         }
     }
     wave_sync();
-    // forward max-fill: occ_sym[j] = owner of positive occurrence j
+    // forward max-fill: occ_sym[j] = owner of positive occurrence j (4 per
+    // lane; entries at and above total_pos are filled too and never read)
     {
+        uint32_t* occ4 = reinterpret_cast<uint32_t*>(occ_sym);
         uint32_t carry = 0;
-        for (uint32_t base = 0; base < total_pos; base += WAVE) {
-            uint32_t j = base + lane;
-            uint32_t v = (j < total_pos) ? occ_sym[j] : 0u;
-            uint32_t f = max(wave_incl_max(v), carry);
-            if (j < total_pos) occ_sym[j] = (uint8_t)f;
-            carry = bcast63(f);
+        for (uint32_t base = 0; base * 4u < total_pos; base += WAVE) {
+            const uint32_t q = base + lane;
+            const uint32_t w = q * 4u < size ? occ4[q] : 0u;
+            const uint32_t m0 = w & 0xFFu, m1 = max(m0, (w >> 8) & 0xFFu), m2 = max(m1, (w >> 16) & 0xFFu),
+                           m3 = max(m2, w >> 24);
+            const uint32_t incl = wave_incl_max(m3);
+            const uint32_t b = max(carry, wave_shr1(incl));
+            if (q * 4u < size) occ4[q] = max(b, m0) | (max(b, m1) << 8) | (max(b, m2) << 16) | (max(b, m3) << 24);
+            carry = max(carry, bcast63(incl));
         }
     }
     wave_sync();
-    // spread: j-th valid multiplier -> position
+    // spread: j-th valid multiplier -> position (multipliers 4q..4q+3 per lane)
     const uint32_t step = (size >> 3) * 5u + 3u;  // table_step: size*5/8+3 (fse.rs:67-70)
     {
         uint32_t j0 = 0;
-        for (uint32_t base = 0; base < size; base += WAVE) {
-            uint32_t m = base + lane;
-            bool act = m < size;
-            uint32_t p = (m * step) & mask;
-            bool valid = act && (int32_t)p <= ht;
-            uint64_t bal = __ballot(valid);
-            uint32_t j = j0 + (uint32_t)__popcll(bal & lanemask_lt());
-            if (valid && j < total_pos) sym_at[p] = occ_sym[j];
-            j0 += (uint32_t)__popcll(bal);
+        for (uint32_t base = 0; base < size; base += 4u * WAVE) {
+            const uint32_t m = base + 4u * lane;
+            uint32_t p[4], nv = 0;
+            bool v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                p[k] = ((m + k) * step) & mask;
+                v[k] = m + k < size && (int32_t)p[k] <= ht;
+                nv += v[k] ? 1u : 0u;
+            }
+            const uint32_t incl = wave_incl_sum(nv);
+            uint32_t j = j0 + incl - nv;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (v[k] && j < total_pos) sym_at[p[k]] = occ_sym[j];
+                j += v[k] ? 1u : 0u;
+            }
+            j0 += bcast63(incl);
         }
         if (j0 != total_pos) return FSE_ERR_BAD_TABLE;  // position != 0 assert
     }
     wave_sync();
+    if (RK != nullptr && tl <= 64u && size >= WAVE) {
+        // pass 1: per 64-position chunk t, each symbol's count at RK[t][s]
+        // (written by its lowest lane) and each lane's peers below, packed
+        // four chunks per register
+        const uint32_t nch = size / WAVE, kb = key_bits(tl);
+        for (uint32_t i = lane; i < nch * 64u / 8u; i += WAVE) reinterpret_cast<uint4*>(RK)[i] = make_uint4(0, 0, 0, 0);
+        wave_sync();
+        uint32_t below[(MAXCH + 3) / 4];
+#pragma unroll
+        for (uint32_t t = 0; t < MAXCH; ++t) {
+            if ((t & 3u) == 0) below[t >> 2] = 0;
+            if (t < nch) {
+                const uint32_t sy = sym_at[t * WAVE + lane];
+                const uint64_t peers = match_key(sy, ~0ull, kb);
+                const uint32_t bl = (uint32_t)__popcll(peers & lanemask_lt());
+                if (bl == 0) RK[t * 64u + sy] = (uint16_t)__popcll(peers);
+                below[t >> 2] |= bl << (8u * (t & 3u));
+            }
+        }
+        wave_sync();
+        // per-symbol exclusive prefix over the chunks (lane = symbol)
+        {
+            uint32_t run = 0;
+#pragma unroll
+            for (uint32_t t = 0; t < MAXCH; ++t) {
+                if (t < nch) {
+                    const uint32_t c = RK[t * 64u + lane];
+                    RK[t * 64u + lane] = (uint16_t)run;
+                    run += c;
+                }
+            }
+        }
+        wave_sync();
+        // pass 2: rank = the symbol's count in earlier chunks + peers below
+#pragma unroll
+        for (uint32_t t = 0; t < MAXCH; ++t) {
+            if (t < nch) {
+                const uint32_t i = t * WAVE + lane;
+                const uint32_t sy = sym_at[i];
+                visit(i, sy, (uint32_t)RK[t * 64u + sy] + ((below[t >> 2] >> (8u * (t & 3u))) & 0xFFu));
+            }
+        }
+        wave_sync();
+        return FSE_OK;
+    }
     // occurrence ranks in ascending position order
     for (uint32_t base = 0; base < size; base += WAVE) {
         uint32_t i = base + lane;

@@ -73,6 +73,7 @@ struct DtParams {
     uint32_t n_blocks;
     uint32_t* dt;      // [n_blocks][1 << lmax] entries (dte_make layout)
     int32_t* dtinfo;   // header bytes | L << 16, or < 0 = status
+    uint32_t debug;    // ablation: bit0 = header parse only, bit1 = no table stores
 };
 
 struct GenParams {

@@ -1761,35 +1761,54 @@ template <int LMAX>
 __global__ __launch_bounds__(64) void dtable_blocks_kernel(DtParams P) {
     constexpr uint32_t SIZE = 1u << LMAX;
     __shared__ int32_t norm[256];
-    __shared__ uint16_t cumul[256];
-    __shared__ uint32_t cnt[256];
     __shared__ __attribute__((aligned(16))) uint8_t sym_at[SIZE];
-    __shared__ __attribute__((aligned(16))) uint8_t occ[SIZE];
+    // the two-pass rank table (2^L u16) reuses the occurrence owners, the
+    // counters and cumul: all three are dead once the spread walk is done
+    // (the decoder's visit reads norm only); 7 KB per workgroup at L = 11
+    __shared__ __attribute__((aligned(16))) uint16_t rk[SIZE];
+    static_assert(SIZE + 256 * 4 + 256 * 2 <= SIZE * 2, "rank table must cover occ, cnt and cumul");
+    uint8_t* occ = reinterpret_cast<uint8_t*>(rk);
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(rk) + SIZE);
+    uint16_t* cumul = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(rk) + SIZE + 1024);
     const uint32_t lane = lane_id();
     const uint64_t gb = blockIdx.x;
     if (gb >= P.n_blocks) return;
     const uint8_t* in = P.in + gb * P.slot_bytes;
     const uint32_t clen = P.comp_len[gb];
     const uint32_t* w = reinterpret_cast<const uint32_t*>(in);
+    // The header words are loaded before the length arrives when the slot
+    // holds HDR_MAX bytes (always, for encoder slots), so the two loads and
+    // the marker byte's load overlap instead of following one another;
+    // words past the block are zeroed once the length is known.
+    uint32_t r0, r1;
+    if (P.slot_bytes >= HDR_MAX) {
+        r0 = w[lane];
+        r1 = w[lane + 64u];
+    }
+    const uint32_t last = (clen && clen <= P.slot_bytes) ? in[clen - 1u] : 0u;
     const uint32_t nw = (uint32_t)min((uint64_t)min(clen, HDR_MAX) + 3u, P.slot_bytes) >> 2;
-    const uint32_t r0 = lane < nw ? w[lane] : 0u;
-    const uint32_t r1 = lane + 64u < nw ? w[lane + 64u] : 0u;
+    if (P.slot_bytes < HDR_MAX) {
+        r0 = lane < nw ? w[lane] : 0u;
+        r1 = lane + 64u < nw ? w[lane + 64u] : 0u;
+    }
+    r0 = lane < nw ? r0 : 0u;
+    r1 = lane + 64u < nw ? r1 : 0u;
     for (uint32_t s = lane; s < 256u; s += WAVE) norm[s] = 0;
     wave_sync();
     uint32_t L = 0, tl = 0;
     const int hl = header_read_wave(r0, r1, clen, (uint32_t)LMAX, norm, &L, &tl);
     int rc = hl < 0 ? hl : FSE_OK;
-    if (rc == FSE_OK && ((uint32_t)hl >= clen || in[clen - 1] == 0)) rc = FSE_ERR_NO_MARKER;  // lib.rs:222
+    if (rc == FSE_OK && ((uint32_t)hl >= clen || last == 0)) rc = FSE_ERR_NO_MARKER;  // lib.rs:222
     wave_sync();
-    if (rc == FSE_OK) {
+    if (rc == FSE_OK && !(P.debug & 1u)) {
         const uint32_t size = 1u << L;
         uint32_t* dt = P.dt + gb * (uint64_t)SIZE;
-        rc = wave_build_spread(norm, L, tl, sym_at, occ, cumul, cnt, [&](uint32_t i, uint32_t s, uint32_t r) {
+        rc = wave_build_spread<SIZE / 64u>(norm, L, tl, sym_at, occ, cumul, cnt, [&](uint32_t i, uint32_t s, uint32_t r) {
             const int32_t v = norm[s];
             const uint32_t nx = (v < 0 ? 1u : (uint32_t)v) + r;
             const uint32_t nb = L - ilog2u(nx);
-            dt[i] = dte_make(nb, s, (nx << nb) - size);
-        });
+            if (!(P.debug & 2u)) dt[i] = dte_make(nb, s, (nx << nb) - size);
+        }, rk);
     }
     if (lane == 0) P.dtinfo[gb] = rc == FSE_OK ? (int32_t)((uint32_t)hl | (L << 16)) : rc;
 }
