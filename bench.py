@@ -4,16 +4,25 @@
 One step = encode 1 GiB of synthetic bytes (16384 x 64 KiB blocks, LUT
 generator p=0.155, H ~ 4.02 bits/symbol) into reference-exact fse_compress2
 blocks + decode them back, inputs resident in HBM.  N GPUs = N independent
-1 GiB shards (weak scaling, no data-path collective).  Rank 0 prints one
-JSON line.  Launch N>1 with torch.distributed.run (one rank per GPU).
+1 GiB shards (weak scaling, no data-path collective; --strong: 1 GiB in total
+split over the N GPUs).  Rank 0 prints one JSON line.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu]
+`--gpus N` (N > 1) without a torch.distributed.run environment starts the N
+ranks itself: a child `python -m torch.distributed.run --nproc-per-node N`
+launched before this process touches the GPU, one rank per GPU over RCCL.
+With N > 1 the compressed shards are then gathered to rank 0 (gatherv) and
+scattered back for decode, timed separately from `value` (C4).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--strong] [--no-cpu]
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -31,7 +40,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--bytes", type=int, default=1 << 30, help="raw bytes per GPU")
+    ap.add_argument("--bytes", type=int, default=1 << 30,
+                    help="raw bytes per GPU (weak scaling) or in total (--strong)")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: --bytes in total, split by blocks over the ranks")
     ap.add_argument("--block", type=int, default=65536)
     ap.add_argument("--prob", type=float, default=0.155)
     ap.add_argument("--kind", type=int, default=0)
@@ -42,15 +54,62 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-c3", action="store_true", help="skip the decode-only (prebuilt tables) line")
+    ap.add_argument("--c3-blocks", type=int, default=32768,
+                    help="C3 size: blocks of C2 data (32768 x 64 KiB ~ 1 GiB compressed, SURVEY 8(d))")
     ap.add_argument("--no-sweep", action="store_true", help="skip the C5 distribution / table-log sweep")
     ap.add_argument("--sweep-bytes", type=int, default=256 << 20, help="raw bytes per C5 sweep point")
     ap.add_argument("--host", action="store_true",
                     help="also time the host-streaming pipeline (pinned host buffers, PCIe copies overlapped "
                          "with the kernels); reported separately, never in value")
-    ap.add_argument("--gather", action="store_true",
-                    help="after the timed steps, pack each rank's blocks on the GPU and gather the "
-                         "compressed streams to rank 0 (RCCL); reported separately, never in value")
+    ap.add_argument("--no-gather", action="store_true",
+                    help="N > 1: skip the gather of the compressed shards to rank 0 and the scatter back "
+                         "(reported separately, never in value)")
+    ap.add_argument("--scheme", default="round_robin", choices=("round_robin", "contiguous"),
+                    help="block -> rank mapping of the gather/scatter (C4: block b on GPU b mod N)")
     return ap.parse_args()
+
+
+def self_launch(args) -> None:
+    """`--gpus N` outside torch.distributed.run: run the N ranks as a child
+    torch.distributed.run (this process has not touched the GPU: only argparse
+    ran) and exit with its status."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    sys.exit(subprocess.call(cmd, env=env))
+
+
+def host_cpu() -> dict:
+    """Host cores for the CPU baseline: this process's CPU affinity (`nproc`),
+    the cgroup CPU quota if one is set, and the CPU model."""
+    try:
+        n_aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n_aff = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"nproc": n_aff, "cgroup_cpu_quota": quota, "model": model}
 
 
 def workload_name(args, n: int) -> str:
@@ -59,20 +118,42 @@ def workload_name(args, n: int) -> str:
     c2 = (args.kind == 0 and args.prob == 0.155 and args.block == 65536 and n == 1 << 30)
     tag = "C2" if c2 else "custom"
     ent = " (H~4.02 bits/sym)" if c2 else ""
-    return (f"{tag}: {n / 2**30:g} GiB per GPU as {-(-n // args.block)} x {args.block // 1024} KiB independent "
+    where = "in total (strong scaling)" if getattr(args, "strong", False) else "per GPU"
+    return (f"{tag}: {n / 2**30:g} GiB {where} as {-(-n // args.block)} x {args.block // 1024} KiB independent "
             f"blocks, {gen} generator p={args.prob}{ent}, encode ({fmt}-exact) + decode")
+
+
+def _median_rate(fn, nbytes: int, budget_s: float) -> float:
+    """Criterion-like: repeat fn in batches for ~budget_s, median bytes/s."""
+    rates = []
+    t_end = time.perf_counter() + budget_s
+    batch = 1
+    while time.perf_counter() < t_end or len(rates) < 5:
+        t0 = time.perf_counter()
+        for _ in range(batch):
+            fn()
+        dt = time.perf_counter() - t0
+        rates.append(batch * nbytes / dt)
+        if dt < 0.02:
+            batch *= 2
+    return float(np.median(rates))
 
 
 def cpu_baseline(src_host: np.ndarray, block: int, budget_s: float) -> dict:
     """The parity oracle (C restatement of the reference, -O3) on host cores.
 
-    Sample: whole 64 KiB blocks of the same C2 data, compressed+decompressed by
-    `threads` pthreads; repeated over the first blocks until ~budget_s of wall
-    time has been spent (bounded), throughput = raw bytes / wall time.
+    (ii) All host cores: whole 64 KiB blocks of the same C2 data,
+    compressed+decompressed by one pthread per core of this process's CPU
+    affinity (`nproc`); repeated over the first blocks until ~budget_s/2 of
+    wall time has been spent, throughput = raw bytes / wall time.
+    (i) Single core, single block (benches/fse_benchmark.rs semantics): C1
+    (64 KiB geometric p=0.5) and the bench-exact 32 KiB LUT p=0.2 block,
+    median of repeated batches.
     """
     from oracle import oracle as O
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
+    host = host_cpu()
+    threads = max(1, host["nproc"])
     n_blocks = len(src_host) // block
     # calibrate on a small slice
     sample = src_host[: block * min(n_blocks, max(threads * 4, 64))]
@@ -89,37 +170,32 @@ def cpu_baseline(src_host: np.ndarray, block: int, budget_s: float) -> dict:
     while wall < budget_s * 0.5 and reps < 8:
         t0 = time.perf_counter()
         comp, lens, slot = O.compress2_blocks(sample, block, threads)
-        tc = time.perf_counter()
         out = O.decompress2_blocks(comp, slot, lens, block, len(sample), threads)
         t1 = time.perf_counter()
         wall += t1 - t0
         total += len(sample)
         reps += 1
     assert np.array_equal(out, sample)
-    # single-core, bench-exact block (benches/fse_benchmark.rs:30-52)
-    b32 = O.generate(0, 0.2, 0x5EED0001, 0, 1 << 15)
-    c32, _ = O.compress2(b32)
-    t0 = time.perf_counter()
-    it = 0
-    while time.perf_counter() - t0 < 1.0:
-        O.compress2(b32)
-        it += 1
-    enc1 = it * len(b32) / (time.perf_counter() - t0)
-    t0 = time.perf_counter()
-    it = 0
-    while time.perf_counter() - t0 < 1.0:
-        O.decompress2(c32, cap=1 << 16)
-        it += 1
-    dec1 = it * len(b32) / (time.perf_counter() - t0)
+    single = {}
+    for name, kind, prob, nb in (("C1_64KiB_geometric_p0.5", 1, 0.5, 1 << 16),
+                                 ("bench_exact_32KiB_lut_p0.2", 0, 0.2, 1 << 15)):
+        blk = O.generate(kind, prob, 0x5EED0001, 0, nb)
+        cblk, _ = O.compress2(blk)
+        assert O.decompress2(cblk, cap=1 << 17) == blk.tobytes()
+        single[name] = {
+            "compressed_ratio": round(len(cblk) / nb, 4),
+            "encode_MiB_s": round(_median_rate(lambda: O.compress2(blk), nb, 1.0) / 2**20, 1),
+            "decode_MiB_s": round(_median_rate(lambda: O.decompress2(cblk, cap=1 << 17), nb, 1.0) / 2**20, 1)}
     return {
         "value": round(total / wall / 2**30, 4),
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
         "sample": f"{reps} x {n_take >> 20} MiB of the same C2 data ({n_take // block} x 64 KiB blocks), "
-                  f"compress2+decompress2 round trip, {threads} pthreads, oracle/fse_oracle.c -O3",
-        "single_core_32KiB_lut0.2": {"encode_MiB_s": round(enc1 / 2**20, 1),
-                                     "decode_MiB_s": round(dec1 / 2**20, 1)},
+                  f"compress2+decompress2 round trip, {threads} pthreads (one per core of the process's "
+                  f"CPU affinity), oracle/fse_oracle.c -O3",
+        "host": host,
+        "single_core": single,
     }
 
 
@@ -170,8 +246,30 @@ def c5_sweep(dev, nbytes: int, block: int, ckpt: int, reps: int = 3) -> list:
     return rows
 
 
+def load_traffic(name: str):
+    """HBM bytes per launch of kernel `name` from profiles/traffic.json
+    (tools/pmc_summary.py over the FETCH_SIZE / WRITE_SIZE passes), or None."""
+    tpath = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(tpath) as f:
+            t = json.load(f).get(name)
+        return int(t["bytes_per_launch"]) if t else None
+    except (OSError, ValueError, KeyError, TypeError):
+        return None
+
+
+def roofline(kernel: str, ms: float, alg_bytes: int, what: str) -> dict:
+    achieved = alg_bytes / (ms * 1e-3) / 1e9
+    return {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(kernel),
+            "traffic_source": "profiles/traffic.json: rocprofv3 FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, "
+                              "per launch (tools/traffic.sh, tools/pmc_summary.py)",
+            "algorithmic_bytes_per_launch": alg_bytes, "timed": what}
+
+
 def main():
     args = parse()
+    self_launch(args)
     import torch
     import torch.distributed as dist
 
@@ -185,18 +283,31 @@ def main():
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
     if world > 1:
+        import datetime
+
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        tmo = datetime.timedelta(seconds=300)
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=tmo)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=tmo)
     cdev = dev if backend == "nccl" else torch.device("cpu")  # where collective tensors live
 
     from entropy_coders_amd import BlockCodec
 
     codec = BlockCodec(block_size=args.block, table_log=args.table_log, ckpt_interval=args.ckpt,
                        device=dev, nstates=args.nstates)
-    n = args.bytes
+    if args.strong:  # --bytes in total: the rank's blocks of the global order (--scheme)
+        from entropy_coders_amd.dist import rank_blocks
+
+        total_blocks = -(-args.bytes // args.block)
+        mine = rank_blocks(total_blocks, rank, world, args.scheme)
+        tail = args.block * total_blocks - args.bytes  # the last global block may be short
+        n = len(mine) * args.block - (tail if total_blocks - 1 in mine else 0)
+        job_bytes = args.bytes
+    else:
+        n = args.bytes
+        job_bytes = world * n
     seed = 0x5EED0002 ^ (rank * 0x1000193)
     src = codec.generate(args.kind, args.prob, seed, n)
     cb = codec.alloc(n)
@@ -214,6 +325,10 @@ def main():
     for _ in range(args.warmup):
         codec.compress_into(src, cb)
         codec.decompress_into(cb, out, dstat)
+    # sentinels: a timed step that wrote nothing cannot pass the checks below
+    out.fill_(0xA5)
+    dstat.fill_(-99)
+    cb["status"].fill_(-99)
     torch.cuda.synchronize(dev)
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
@@ -243,38 +358,68 @@ def main():
           and bool(torch.equal(out, src)))
     comp_bytes = int(cb["comp_len"].to(torch.int64).sum())
     nb = codec.n_blocks(n)
-    def n_ckpt(ln):  # sidecar entries of a block of ln bytes (pairs for 2-state, symbols for 1-state)
-        return (ln // 2) // args.ckpt + 1 if args.nstates == 2 else (ln - 1) // args.ckpt + 1
 
-    side_bytes = 8 * sum(n_ckpt(min(args.block, n - b * args.block)) for b in range(nb)) if args.ckpt else 0
+    def side_bytes_of(n_raw):  # sidecar bytes actually written/read for n_raw bytes of blocks
+        if not args.ckpt:
+            return 0
+        per = (lambda ln: (ln // 2) // args.ckpt + 1) if args.nstates == 2 else (lambda ln: (ln - 1) // args.ckpt + 1)
+        nbk = -(-n_raw // args.block)
+        return 8 * sum(per(min(args.block, n_raw - b * args.block)) for b in range(nbk))
+
+    side_bytes = side_bytes_of(n)
     if world > 1:
         flag = torch.tensor([1 if ok else 0], device=cdev)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         ok = bool(flag.item())
 
-    # C3 (BASELINE configs[2]): decode only, decode tables prebuilt and untimed
+    # C4 exchange (N > 1): gatherv of the compressed shards to rank 0, then the
+    # scatter back for distributed decode; verified by decoding what came back
+    gather_info = None
+    if world > 1 and not args.no_gather:
+        gather_info = c4_exchange(args, codec, cb, src, world, rank, dev, cdev, backend, barrier)
+        ok = ok and gather_info["verified"]
+        flag = torch.tensor([1 if ok else 0], device=cdev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        ok = bool(flag.item())
+
+    # C3 (BASELINE configs[2]): decode only, decode tables prebuilt and untimed,
+    # on its own 32768 blocks of C2 data (~1 GiB compressed)
     c3 = None
-    comp_bytes_pre = int(cb["comp_len"].to(torch.int64).sum())
-    if not args.no_c3:
-        tabs = codec.build_dtables(cb)
+    if not args.no_c3 and world == 1:
+        n3 = args.c3_blocks * args.block
+        del out
+        src3 = codec.generate(args.kind, args.prob, 0x5EED0003, n3)
+        cb3 = codec.alloc(n3)
+        codec.compress_into(src3, cb3)
+        tabs = codec.build_dtables(cb3)
+        out3 = torch.empty(n3, dtype=torch.uint8, device=dev)
+        st3 = torch.zeros(codec.n_blocks(n3), dtype=torch.int32, device=dev)
+        codec.decompress_dt_into(cb3, tabs, out3, st3)  # warm-up
+        out3.fill_(0xA5)
+        st3.fill_(-99)
         torch.cuda.synchronize(dev)
         e3 = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-        codec.decompress_dt_into(cb, tabs, out, dstat)
         e3[0].record(stream)
         for _ in range(args.steps):
-            codec.decompress_dt_into(cb, tabs, out, dstat)
+            codec.decompress_dt_into(cb3, tabs, out3, st3)
         e3[1].record(stream)
         torch.cuda.synchronize(dev)
         c3_ms = e3[0].elapsed_time(e3[1]) / args.steps
-        c3_ok = int(dstat.abs().max()) == 0 and bool(torch.equal(out, src))
-        c3 = {"workload": "C3-style decode only on the blocks above (prebuilt decode tables, untimed): "
-                          f"{comp_bytes_pre / 2**30:.3f} GiB compressed -> {n / 2**30:.3f} GiB",
-              "decode_ms": round(c3_ms, 4), "decode_GiB_s": round(n / (c3_ms * 1e-3) / 2**30, 2),
-              "roofline_frac": None, "verified": c3_ok}
+        c3_ok = int(cb3["status"].abs().max()) == 0 and int(st3.abs().max()) == 0 and bool(torch.equal(out3, src3))
+        comp3 = int(cb3["comp_len"].to(torch.int64).sum())
+        c3_bytes = comp3 + side_bytes_of(n3) + n3  # compressed + sidecar read, raw written
+        c3 = {"workload": f"C3: decode only, {args.c3_blocks} x {args.block // 1024} KiB blocks of C2 data "
+                          f"({comp3 / 2**30:.3f} GiB compressed -> {n3 / 2**30:.3f} GiB), decode tables and "
+                          "sidecar prebuilt and untimed",
+              "decode_ms": round(c3_ms, 4), "decode_GiB_s": round(n3 / (c3_ms * 1e-3) / 2**30, 2),
+              "roofline": roofline("fse_decode_blocks_c3", c3_ms, c3_bytes,
+                                   "decode launches (prebuilt tables), HIP events"),
+              "verified": c3_ok}
         ok = ok and c3_ok
+        del src3, cb3, tabs, out3, st3
 
     host_info = None
-    if args.host:
+    if args.host and world == 1:
         from entropy_coders_amd.stream import HostPipeline
 
         pipe = HostPipeline(codec, chunk_blocks=1024)
@@ -299,75 +444,35 @@ def main():
         ok = ok and h_ok
         del host_src, hs_stream, h_out, c_out, d_out
 
-    gather_info = None
-    if args.gather:
-        from entropy_coders_amd.dist import gather_stream, pack_device
-
-        packed, _ = pack_device(cb["out"], codec.slot_bytes, cb["comp_len"])  # warm-up (allocation)
-        del packed
-        torch.cuda.synchronize(dev)
-        barrier()
-        g0 = time.perf_counter()
-        packed, _ = pack_device(cb["out"], codec.slot_bytes, cb["comp_len"])
-        torch.cuda.synchronize(dev)
-        tp = time.perf_counter()
-        if world > 1:
-            streams, _ = gather_stream(packed, cb["comp_len"], dst=0)
-        torch.cuda.synchronize(dev)
-        g1 = time.perf_counter()
-        gather_info = {"packed_bytes_per_rank": int(packed.numel()),
-                       "pack_ms": round((tp - g0) * 1e3, 3),
-                       "pack_plus_gather_ms": round((g1 - g0) * 1e3, 3),
-                       "gather_GB_s": round(world * packed.numel() / max(g1 - tp, 1e-9) / 1e9, 2)
-                       if world > 1 else None}
-
     if rank == 0:
         enc_bytes = n + comp_bytes + side_bytes  # raw read + compressed (+ sidecar) written
         dec_bytes = comp_bytes + side_bytes + n  # compressed (+ sidecar) read + raw written
-        dom = ("fse_encode_blocks", enc_ms, enc_bytes) if enc_ms >= dec_ms else \
-              ("fse_decode_blocks", dec_ms, dec_bytes)
-        achieved = dom[2] / (dom[1] * 1e-3) / 1e9
-        traffic = None
-        tpath = os.path.join(ROOT, "profiles", "traffic.json")
-        if os.path.exists(tpath):
-            try:
-                with open(tpath) as f:
-                    t = json.load(f).get(dom[0])
-                traffic = int(t["bytes_per_launch"]) if t else None
-            except Exception:
-                traffic = None
         line = {
             "metric": METRIC,
-            "value": round(world * n * args.steps / elapsed / 2**30, 3),
+            "value": round(job_bytes * args.steps / elapsed / 2**30, 3),
             "unit": "GiB/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic",
             "config": {
-                "workload": workload_name(args, n),
+                "workload": workload_name(args, args.bytes if args.strong else n),
                 "format": "2-state (fse_compress2)" if args.nstates == 2 else "1-state (fse_compress)",
                 "block_size": args.block,
+                "bytes_per_gpu": n,
                 "table_log": args.table_log or "optimal (11)",
                 "ckpt_interval": f"{args.ckpt} {'pairs' if args.nstates == 2 else 'symbols'}",
                 "parallelism": f"dp{world} (blocks sharded per GPU, no collective in the step)",
             },
-            "roofline": {
-                "bound": "hbm",
-                "kernel": dom[0],
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "traffic_source": "profiles/traffic.json: rocprofv3 FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, per launch",
-                "algorithmic_bytes_per_launch": dom[2],
-            },
+            # dominant kernel of the step: encode (one launch per step)
+            "roofline": roofline("fse_encode_blocks", enc_ms, enc_bytes, "encode launch, HIP events"),
+            "roofline_decode": roofline("fse_decode_blocks", dec_ms, dec_bytes,
+                                        "decode-table + decode launches, HIP events"),
             "encode_ms": round(enc_ms, 4),
             "decode_ms": round(dec_ms, 4),
             "encode_GiB_s": round(n / (enc_ms * 1e-3) / 2**30, 2),
@@ -375,14 +480,15 @@ def main():
             "compressed_ratio": round(comp_bytes / n, 5),
             "verified_roundtrip": ok,
         }
+        if enc_ms < dec_ms:
+            line["roofline"], line["roofline_decode"] = line["roofline_decode"], line["roofline"]
         if c3 is not None:
-            c3["roofline_frac"] = round(dec_bytes / (c3["decode_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
             line["c3_decode_only"] = c3
         if gather_info is not None:
-            line["gather"] = gather_info
+            line["c4_exchange"] = gather_info
         if host_info is not None:
             line["host_pipeline"] = host_info
-        if not args.no_sweep and args.nstates == 2:
+        if not args.no_sweep and args.nstates == 2 and world == 1:
             sw = c5_sweep(dev, args.sweep_bytes, args.block, args.ckpt)
             line["c5_sweep"] = {"workload": f"C5: {args.sweep_bytes >> 20} MiB per distribution and table log, "
                                             "encode + decode (2-state), 1 GPU", "rows": sw}
@@ -395,6 +501,81 @@ def main():
         dist.destroy_process_group()
     if not ok:
         sys.exit(3)
+
+
+def c4_exchange(args, codec, cb, src, world, rank, dev, cdev, backend, barrier) -> dict:
+    """BASELINE configs[3] / SURVEY 8(e): pack each rank's blocks on the GPU,
+    gatherv them (lengths, bytes, sidecar) to rank 0 over RCCL, then scatter
+    the global stream back and decode each rank's received shard.  Timed
+    separately from `value`; the gather is reported as achieved GB/s into
+    rank 0 against the 7-link xGMI ingress roof."""
+    import torch
+
+    from entropy_coders_amd.dist import (concat_global, gather_stream, pack_device, scatter_stream,
+                                         unpack_device)
+
+    nb = codec.n_blocks(cb["n_total"])
+    side = cb["sidecar"][: nb * codec.side_per_block] if args.ckpt else None
+    to_c = (lambda t: t) if backend == "nccl" else (lambda t: t.cpu() if t is not None else None)
+
+    packed, _ = pack_device(cb["out"], codec.slot_bytes, cb["comp_len"])
+    torch.cuda.synchronize(dev)
+    barrier()
+    g0 = time.perf_counter()
+    packed, _ = pack_device(cb["out"], codec.slot_bytes, cb["comp_len"])
+    torch.cuda.synchronize(dev)
+    tp = time.perf_counter()
+    res = gather_stream(to_c(packed), to_c(cb["comp_len"]), dst=0, sidecar=to_c(side))
+    torch.cuda.synchronize(dev)
+    barrier()
+    g1 = time.perf_counter()
+    streams, lens, sides = res
+    recv_bytes = 0
+    g_stream = g_lens = g_side = None
+    n_global = 0
+    sizes = torch.tensor([nb], dtype=torch.int64, device=cdev)
+    allnb = [torch.zeros_like(sizes) for _ in range(world)]
+    import torch.distributed as dist
+
+    dist.all_gather(allnb, sizes)
+    n_global = int(sum(int(x) for x in allnb))
+    if rank == 0:
+        recv_bytes = sum(int(s.numel()) for r, s in enumerate(streams) if r != 0)
+        recv_bytes += sum(int(s.numel()) * 8 for r, s in enumerate(sides) if r != 0 and s is not None)
+        g_stream, g_lens, g_side = concat_global(streams, lens, n_global, world, args.scheme,
+                                                 sides if side is not None else None)
+    torch.cuda.synchronize(dev)
+    barrier()
+    s0 = time.perf_counter()
+    my, my_lens, my_side, idx = scatter_stream(g_stream, g_lens, src=0, sidecar=g_side,
+                                               side_per_block=codec.side_per_block, scheme=args.scheme,
+                                               device=cdev)
+    torch.cuda.synchronize(dev)
+    barrier()
+    s1 = time.perf_counter()
+    # decode what came back: rank r's j-th block of the global order is its local block j
+    my, my_lens = my.to(dev), my_lens.to(dev)
+    slots = unpack_device(my, my_lens, codec.slot_bytes)
+    cb2 = {"n_total": cb["n_total"], "out": slots, "comp_len": my_lens,
+           "sidecar": my_side.to(dev) if my_side is not None else cb["sidecar"]}
+    out2 = torch.full((cb["n_total"],), 0xA5, dtype=torch.uint8, device=dev)
+    st2 = torch.full((nb,), -99, dtype=torch.int32, device=dev)
+    codec.decompress_into(cb2, out2, st2, use_sidecar=my_side is not None)
+    torch.cuda.synchronize(dev)
+    ok = (len(idx) == nb and int(st2.abs().max()) == 0 and bool(torch.equal(out2, src))
+          and bool(torch.equal(my_lens.cpu(), cb["comp_len"].cpu())))
+    xgmi_roof = 153.0 * min(world - 1, 7)
+    gather_gbs = recv_bytes / max(g1 - tp, 1e-9) / 1e9
+    return {"scheme": args.scheme, "backend": backend,
+            "packed_bytes_rank0": int(packed.numel()),
+            "gathered_bytes_into_rank0": recv_bytes,
+            "pack_ms": round((tp - g0) * 1e3, 3),
+            "gather_ms": round((g1 - tp) * 1e3, 3),
+            "gather_GB_s_into_rank0": round(gather_gbs, 2),
+            "xgmi_ingress_roof_GB_s": xgmi_roof,
+            "gather_roof_frac": round(gather_gbs / xgmi_roof, 4) if backend == "nccl" else None,
+            "scatter_ms": round((s1 - s0) * 1e3, 3),
+            "verified": ok}
 
 
 if __name__ == "__main__":

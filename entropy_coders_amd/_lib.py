@@ -23,6 +23,7 @@ EXPORTS = (
     "fsehip_pack_blocks", "fsehip_unpack_blocks",
     "fsehip_dtable_bytes", "fsehip_build_dtables", "fsehip_decompress_blocks_dt",
     "fse_compress", "fse_decompress", "fsehip_sidecar_per_block_ns",
+    "fsehip_copy_blocks",
 )
 
 STATUS = {
@@ -83,6 +84,7 @@ def load() -> C.CDLL:
     lib.fsehip_generate.argtypes = [C.c_int, C.c_double, u64, u32, P, u64, P]
     lib.fsehip_pack_blocks.argtypes = [P, u64, P, P, u32, P, P]
     lib.fsehip_unpack_blocks.argtypes = [P, P, P, u32, P, u64, P]
+    lib.fsehip_copy_blocks.argtypes = [P, P, P, u32, P, P, P]
     lib.fsehip_device_count.argtypes = []
     lib.fsehip_version.restype = C.c_char_p
     for name in EXPORTS:

@@ -479,6 +479,16 @@ int fsehip_unpack_blocks(const uint8_t* d_stream, const uint64_t* d_offsets, con
     return e == hipSuccess ? FSE_OK : FSE_ERR_HIP;
 }
 
+int fsehip_copy_blocks(const uint8_t* d_src, const uint64_t* d_src_offsets, const uint32_t* d_lens, uint32_t n_blocks,
+                       uint8_t* d_dst, const uint64_t* d_dst_offsets, fsehip_stream_t stream) {
+    if (n_blocks == 0) return FSE_OK;
+    if (!d_src || !d_src_offsets || !d_lens || !d_dst || !d_dst_offsets) return FSE_ERR_BAD_ARG;
+    if (!device_ok()) return FSE_ERR_NO_DEVICE;
+    hipError_t e = fsehip::launch_copy(d_src, d_src_offsets, d_lens, n_blocks, d_dst, d_dst_offsets,
+                                       static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? FSE_OK : FSE_ERR_HIP;
+}
+
 int fsehip_generate(int kind, double prob, uint64_t seed, uint32_t block_size, uint8_t* d_out, uint64_t n_total,
                     fsehip_stream_t stream) {
     if (!d_out || kind < 0 || kind > 2) return FSE_ERR_BAD_ARG;

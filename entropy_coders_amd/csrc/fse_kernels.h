@@ -99,5 +99,7 @@ hipError_t launch_histogram(const uint8_t* src, uint64_t n_total, uint32_t block
 hipError_t launch_generate(const GenParams& G, hipStream_t stream);
 hipError_t launch_pack(const uint8_t* slots, uint64_t slot_bytes, const uint32_t* comp_len, const uint64_t* offsets,
                        uint32_t n_blocks, uint8_t* stream, int unpack, hipStream_t hs);
+hipError_t launch_copy(const uint8_t* src, const uint64_t* src_off, const uint32_t* lens, uint32_t n_blocks,
+                       uint8_t* dst, const uint64_t* dst_off, hipStream_t hs);
 
 }  // namespace fsehip

@@ -2093,6 +2093,42 @@ __global__ __launch_bounds__(256) void pack_blocks_kernel(const uint8_t* __restr
 }
 
 // ------------------------------------------------------------------------
+// Byte-range gather between two packed streams: block b's len[b] bytes move
+// from src + src_off[b] to dst + dst_off[b] (both arbitrary byte offsets).
+// Selects a rank's blocks out of a packed stream for the distributed
+// scatter (round-robin shards are not contiguous in the global stream).
+// Destination dwords come from two aligned source dwords (v_alignbyte); the
+// partial dwords at either end, shared with neighbouring blocks, bytewise.
+// ------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void copy_blocks_kernel(const uint8_t* __restrict__ src,
+                                                          const uint64_t* __restrict__ src_off,
+                                                          const uint32_t* __restrict__ lens, uint32_t n_blocks,
+                                                          uint8_t* __restrict__ dst,
+                                                          const uint64_t* __restrict__ dst_off) {
+    const uint64_t b = blockIdx.x;
+    if (b >= n_blocks) return;
+    const uint32_t len = lens[b];
+    const uint64_t so = src_off[b], o = dst_off[b];
+    const uint64_t d0 = (o + 3u) >> 2, d1 = (o + len) >> 2;  // whole destination dwords [d0, d1)
+    uint32_t* dw = reinterpret_cast<uint32_t*>(dst);
+    if (d1 > d0) {
+        const uint64_t s0 = so + (4u * d0 - o);  // source byte feeding dword d0
+        const uint32_t sh = (uint32_t)(s0 & 3u);
+        const uint32_t* sw = reinterpret_cast<const uint32_t*>(src) + (s0 >> 2);
+        for (uint64_t d = threadIdx.x; d < d1 - d0; d += 256u) {
+            const uint32_t lo = sw[d];
+            // the word above is read only when it carries bytes of this block
+            const uint32_t hi = sh ? sw[d + 1u] : 0u;
+            dw[d0 + d] = __builtin_amdgcn_alignbyte(hi, lo, sh);
+        }
+    }
+    const uint64_t hb = min((uint64_t)len, 4u * d0 - o);
+    if (threadIdx.x < hb) dst[o + threadIdx.x] = src[so + threadIdx.x];
+    const uint64_t tb0 = d1 > d0 ? 4u * d1 - o : hb;
+    for (uint64_t i = tb0 + threadIdx.x; i < len; i += 256u) dst[o + i] = src[so + i];
+}
+
+// ------------------------------------------------------------------------
 // Synthetic generator (same definition as oracle fo_generate).
 // ------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
@@ -2289,6 +2325,13 @@ hipError_t launch_pack(const uint8_t* slots, uint64_t slot_bytes, const uint32_t
                        uint32_t n_blocks, uint8_t* stream, int unpack, hipStream_t hs) {
     hipLaunchKernelGGL(pack_blocks_kernel, dim3(n_blocks), dim3(256), 0, hs, slots, slot_bytes, comp_len, offsets,
                        n_blocks, stream, unpack);
+    return hipGetLastError();
+}
+
+hipError_t launch_copy(const uint8_t* src, const uint64_t* src_off, const uint32_t* lens, uint32_t n_blocks,
+                       uint8_t* dst, const uint64_t* dst_off, hipStream_t hs) {
+    hipLaunchKernelGGL(copy_blocks_kernel, dim3(n_blocks), dim3(256), 0, hs, src, src_off, lens, n_blocks, dst,
+                       dst_off);
     return hipGetLastError();
 }
 

@@ -135,6 +135,13 @@ int fsehip_pack_blocks(const uint8_t* d_slots, uint64_t slot_bytes, const uint32
 int fsehip_unpack_blocks(const uint8_t* d_stream, const uint64_t* d_offsets, const uint32_t* d_comp_len,
                          uint32_t n_blocks, uint8_t* d_slots, uint64_t slot_bytes, fsehip_stream_t stream);
 
+/* Move whole blocks between packed streams: block b's d_lens[b] bytes go from
+ * d_src + d_src_offsets[b] to d_dst + d_dst_offsets[b] (any byte offsets;
+ * ranges must not overlap).  Selects one rank's blocks out of a packed
+ * stream for the distributed scatter (entropy_coders_amd/dist.py). */
+int fsehip_copy_blocks(const uint8_t* d_src, const uint64_t* d_src_offsets, const uint32_t* d_lens, uint32_t n_blocks,
+                       uint8_t* d_dst, const uint64_t* d_dst_offsets, fsehip_stream_t stream);
+
 /* histogram::count per block: d_counts[b*256 + s], d_table_len[b]. */
 int fsehip_histogram_blocks(const uint8_t* d_src, uint64_t n_total, uint32_t block_size, uint32_t* d_counts,
                             uint32_t* d_table_len, fsehip_stream_t stream);

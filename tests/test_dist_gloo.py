@@ -1,6 +1,8 @@
-"""world_size-2 gloo tests of the multi-GPU path on CPU: block sharding and
-the compressed-output gather (the only collective), with blocks produced by
-the CPU oracle (test checker) standing in for each rank's GPU output."""
+"""world_size-2 (and 3) gloo tests of the multi-GPU exchange on CPU: block
+sharding, the compressed-output gatherv and the scatter for distributed
+decode, with blocks produced by the CPU oracle (test checker) standing in for
+each rank's GPU output.  The same functions run over RCCL on MI355X
+(tests/test_gpu_dist.py drives them with the HIP encoder's blocks)."""
 import os
 import socket
 
@@ -10,9 +12,10 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from entropy_coders_amd.dist import assemble, gather_stream, pack_host, rank_blocks
+from entropy_coders_amd.dist import (assemble, concat_global, gather_stream, pack_host, rank_blocks,
+                                     scatter_stream)
 
-N_BLOCKS, BLOCK = 11, 4096
+N_BLOCKS, BLOCK, SPB = 11, 4096, 5
 
 
 def _free_port():
@@ -23,6 +26,17 @@ def _free_port():
     return p
 
 
+def _block(b):
+    from oracle import oracle as O
+
+    # per-block distribution varies, so shards have different byte sizes
+    return O.generate(0, 0.1 + 0.05 * (b % 5), 42, b, BLOCK)
+
+
+def _fake_sidecar(b):
+    return torch.arange(SPB, dtype=torch.int64) + 1000 * b
+
+
 def _worker(rank, world, port, scheme, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -31,40 +45,58 @@ def _worker(rank, world, port, scheme, q):
         from oracle import oracle as O
 
         mine = list(rank_blocks(N_BLOCKS, rank, world, scheme))
-        slot = O.compress_bound(BLOCK) + 16
-        slot = (slot + 15) // 16 * 16
+        slot = (O.compress_bound(BLOCK) + 16 + 15) // 16 * 16
         slots = torch.zeros(max(len(mine), 1) * slot, dtype=torch.uint8)
         lens = torch.zeros(len(mine), dtype=torch.int32)
+        side = torch.cat([_fake_sidecar(b) for b in mine]) if mine else torch.zeros(0, dtype=torch.int64)
         for j, b in enumerate(mine):
-            src = O.generate(0, 0.2, 42, b, BLOCK)
-            comp, _ = O.compress2(src)
+            comp, _ = O.compress2(_block(b))
             slots[j * slot: j * slot + len(comp)] = torch.from_numpy(np.frombuffer(comp, np.uint8).copy())
             lens[j] = len(comp)
         stream, _ = pack_host(slots, slot, lens)
-        streams, all_lens = gather_stream(stream, lens, dst=0)
+        streams, all_lens, sides = gather_stream(stream, lens, dst=0, sidecar=side)
+        ok = True
+        g_stream = g_lens = g_side = None
         if rank == 0:
             index = assemble(streams, all_lens, N_BLOCKS, world, scheme)
-            ok = True
             for b, (r, off, ln) in enumerate(index):
                 got = streams[r][off: off + ln].numpy().tobytes()
-                want = O.compress2(O.generate(0, 0.2, 42, b, BLOCK))[0]
-                ok &= got == want
-                ok &= O.decompress2(got, raw_len=BLOCK) == O.generate(0, 0.2, 42, b, BLOCK).tobytes()
-            q.put(ok)
+                ok &= got == O.compress2(_block(b))[0]
+                ok &= O.decompress2(got, raw_len=BLOCK) == _block(b).tobytes()
+            g_stream, g_lens, g_side = concat_global(streams, all_lens, N_BLOCKS, world, scheme, sides)
+            want_side = torch.cat([_fake_sidecar(b) for b in range(N_BLOCKS)])
+            ok &= bool(torch.equal(g_side, want_side))
+        else:
+            ok &= streams is None and all_lens is None and sides is None
+        # the reverse: rank 0 scatters the global stream, each rank checks its blocks
+        s, l, sc, idx = scatter_stream(g_stream, g_lens, src=0, sidecar=g_side, side_per_block=SPB,
+                                       scheme=scheme, device="cpu")
+        ok &= list(idx) == mine and len(l) == len(mine)
+        o = 0
+        for j, b in enumerate(mine):
+            ln = int(l[j])
+            ok &= s[o:o + ln].numpy().tobytes() == O.compress2(_block(b))[0]
+            o += ln
+            ok &= bool(torch.equal(sc[j * SPB:(j + 1) * SPB], _fake_sidecar(b)))
+        ok &= o == s.numel()
+        flag = torch.tensor([1 if ok else 0])
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if rank == 0:
+            q.put(bool(flag.item()))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("scheme", ["contiguous", "round_robin"])
-def test_gather_two_ranks(scheme):
+@pytest.mark.parametrize("scheme,world", [("contiguous", 2), ("round_robin", 2), ("round_robin", 3)])
+def test_gather_scatter(scheme, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, scheme, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, scheme, q)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
-        p.join(120)
+        p.join(180)
         assert p.exitcode == 0
     assert q.get(timeout=10) is True
 

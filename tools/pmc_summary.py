@@ -1,8 +1,12 @@
-"""Summarise rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/traffic.sh) into
-per-launch HBM bytes for the fse kernels, with the gfx950 corrections of
-MI355X_MICROARCH.md (HBM section): counters are in KiB; FETCH_SIZE reports
-half the bytes of wide coalesced reads, so it is doubled (upper bound for
-narrower access); WRITE_SIZE is taken as reported.
+"""Summarise rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/traffic.sh over
+tools/prof_bench.py) into per-launch HBM bytes for the fse kernels, with the
+gfx950 corrections of MI355X_MICROARCH.md (HBM section): counters are in
+KiB; FETCH_SIZE reports half the bytes of wide coalesced reads, so it is
+doubled (upper bound for narrower access); WRITE_SIZE is taken as reported.
+
+Launches are told apart by kernel name and grid (workgroups): C2 runs 16384
+blocks, C3 32768; the decode's second launch (66 KiB stage, 67584u) only
+decodes blocks deferred by the first, none on C2 data.
 
     python tools/pmc_summary.py gpurun_out/traffic [--json profiles/traffic.json]
 """
@@ -12,10 +16,23 @@ import json
 import sys
 from collections import defaultdict
 
-KERNELS = {"encode_blocks_kernel": "fse_encode_blocks", "decode_blocks_kernel": "fse_decode_blocks_fused",
-           "decode_pre_kernel": "fse_decode_blocks", "dtable_blocks_kernel": "fse_build_dtables",
-           "decode1_serial_kernel": "fse_decode1_serial",
-           "pack_blocks_kernel": "fse_pack_blocks", "generate_kernel": "fse_generate"}
+
+def classify(kernel: str, groups: int):
+    c3 = groups == 32768
+    if "encode_blocks_kernel" in kernel:
+        return "fse_encode_blocks" + ("_c3_input" if c3 else "")
+    if "dtable_blocks_kernel" in kernel:
+        return "fse_build_dtables" + ("_c3" if c3 else "")
+    if "decode_pre_kernel" in kernel:
+        if "67584u" in kernel:
+            return "fse_decode_deferred" + ("_c3" if c3 else "")
+        return "fse_decode_blocks" + ("_c3" if c3 else "")
+    for k, name in (("serial2_decode_kernel", "fse_decode_serial2"), ("decode_blocks_kernel", "fse_decode_fused"),
+                    ("decode1_serial_kernel", "fse_decode1_serial"), ("pack_blocks_kernel", "fse_pack_blocks"),
+                    ("copy_blocks_kernel", "fse_copy_blocks"), ("generate_kernel", "fse_generate")):
+        if k in kernel:
+            return name
+    return None
 
 
 def load(d, counter):
@@ -24,9 +41,10 @@ def load(d, counter):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
-            for k, name in KERNELS.items():
-                if k in r["Kernel_Name"]:
-                    vals[name].append(float(r["Counter_Value"]) * 1024.0)
+            groups = int(r["Grid_Size"]) // max(int(r["Workgroup_Size"]), 1)
+            name = classify(r["Kernel_Name"], groups)
+            if name:
+                vals[name].append(float(r["Counter_Value"]) * 1024.0)
     return vals
 
 
@@ -41,13 +59,13 @@ def main():
         # last launch of each kind (the first may see a cold Infinity Cache)
         fb = 2.0 * f[-1] if f else None
         wb = w[-1] if w else None
-        out[name] = {"fetch_bytes_corrected": fb, "fetch_bytes_raw": f[-1] if f else None,
-                     "write_bytes": wb, "hbm_bytes": (fb or 0) + (wb or 0), "launches": max(len(f), len(w))}
+        out[name] = {"bytes_per_launch": (fb or 0) + (wb or 0), "fetch_bytes_corrected": fb,
+                     "fetch_bytes_raw": f[-1] if f else None, "write_bytes": wb, "launches": max(len(f), len(w))}
         print(name, json.dumps(out[name]))
     if "--json" in sys.argv:
         path = sys.argv[sys.argv.index("--json") + 1]
         with open(path, "w") as fh:
-            json.dump({k: {"bytes_per_launch": v["hbm_bytes"], **v} for k, v in out.items()}, fh, indent=1)
+            json.dump(out, fh, indent=1)
 
 
 if __name__ == "__main__":
