@@ -24,13 +24,17 @@ EXPORTS = (
     "fsehip_dtable_bytes", "fsehip_build_dtables", "fsehip_decompress_blocks_dt",
     "fse_compress", "fse_decompress", "fsehip_sidecar_per_block_ns",
     "fsehip_copy_blocks",
+    "histogram_new", "histogram_normalize", "histogram_normalize_optimal", "norm_histogram_new",
+    "norm_histogram_write", "norm_histogram_read", "encode_table_new", "decode_table_new", "fse_compress_nh",
+    "bitstack_write", "bitstack_read", "bitstream_read",
+    "fsehip_bitstack_write", "fsehip_bitstack_read", "fsehip_bitstream_read",
 )
 
 STATUS = {
     0: "OK", -1: "EMPTY", -2: "TOO_SHORT", -3: "ALL_ZERO_SYMBOL0", -4: "SINGLE_SYMBOL",
     -5: "BAD_HEADER", -6: "NO_MARKER", -7: "DST_TOO_SMALL", -8: "TABLELOG_RANGE",
     -9: "CURSED", -10: "BAD_TABLE", -11: "BAD_ARG", -12: "HIP", -13: "LENGTH_MISMATCH",
-    -14: "UNSUPPORTED", -15: "NO_DEVICE",
+    -14: "UNSUPPORTED", -15: "NO_DEVICE", -16: "BAD_SIDECAR", -17: "ENCODER_INIT",
 }
 
 
@@ -47,6 +51,35 @@ class Params(C.Structure):
     _fields_ = [("block_size", C.c_uint32), ("table_log", C.c_uint32),
                 ("ckpt_interval", C.c_uint32), ("max_table_log", C.c_uint32),
                 ("nstates", C.c_uint32)]
+
+
+class Histogram(C.Structure):
+    """fse_histogram = Histogram (histogram.rs:9-14)."""
+    _fields_ = [("counts", C.c_uint32 * 256), ("size", C.c_uint32), ("table_len", C.c_uint32)]
+
+
+class NormHistogram(C.Structure):
+    """fse_norm_histogram = NormHistogram (histogram.rs:289-294)."""
+    _fields_ = [("norm", C.c_int32 * 256), ("log2", C.c_uint32), ("table_len", C.c_uint32)]
+
+
+class SymbolTransform(C.Structure):
+    _fields_ = [("bits", C.c_uint32), ("find_state", C.c_int32)]
+
+
+class EncodeTable(C.Structure):
+    """fse_encode_table = EncodeTable (fse.rs:72-84)."""
+    _fields_ = [("table_log", C.c_uint32), ("table", C.c_uint16 * 32768), ("symbols", C.c_uint8 * 32768),
+                ("symbol_tt", SymbolTransform * 256)]
+
+
+class DecodeTransform(C.Structure):
+    _fields_ = [("new_state", C.c_uint16), ("symbol", C.c_uint8), ("num_bits", C.c_uint8)]
+
+
+class DecodeTable(C.Structure):
+    """fse_decode_table = DecodeTable (fse.rs:253-265)."""
+    _fields_ = [("table_log", C.c_uint32), ("fast_mode", C.c_uint32), ("table", DecodeTransform * 32768)]
 
 
 _lib = None
@@ -85,6 +118,22 @@ def load() -> C.CDLL:
     lib.fsehip_pack_blocks.argtypes = [P, u64, P, P, u32, P, P]
     lib.fsehip_unpack_blocks.argtypes = [P, P, P, u32, P, u64, P]
     lib.fsehip_copy_blocks.argtypes = [P, P, P, u32, P, P, P]
+    H, NH = C.POINTER(Histogram), C.POINTER(NormHistogram)
+    lib.histogram_new.argtypes = [P, sz, H]
+    lib.histogram_normalize.argtypes = [H, u32, NH]
+    lib.histogram_normalize_optimal.argtypes = [H, NH]
+    lib.norm_histogram_new.argtypes = [P, sz, NH]
+    lib.norm_histogram_write.argtypes = [NH, P, sz, C.POINTER(sz), C.POINTER(u64)]
+    lib.norm_histogram_read.argtypes = [P, sz, NH, C.POINTER(sz)]
+    lib.encode_table_new.argtypes = [NH, C.POINTER(EncodeTable)]
+    lib.decode_table_new.argtypes = [NH, C.POINTER(DecodeTable)]
+    lib.fse_compress_nh.argtypes = [P, sz, P, sz, C.POINTER(sz), C.POINTER(u64), NH]
+    lib.bitstack_write.argtypes = [P, P, sz, P, sz, C.POINTER(sz), C.POINTER(u64)]
+    lib.bitstack_read.argtypes = [P, sz, P, sz, P, C.POINTER(sz), C.POINTER(C.c_int)]
+    lib.bitstream_read.argtypes = [P, sz, u64, P, sz, P, C.POINTER(sz), C.POINTER(u64)]
+    lib.fsehip_bitstack_write.argtypes = [P, P, u64, P, u64, P, P]
+    lib.fsehip_bitstack_read.argtypes = [P, u64, P, u64, P, P, P]
+    lib.fsehip_bitstream_read.argtypes = [P, u64, u64, P, u64, P, P, P]
     lib.fsehip_device_count.argtypes = []
     lib.fsehip_version.restype = C.c_char_p
     for name in EXPORTS:

@@ -10,6 +10,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <memory>
 #include <mutex>
 #include <vector>
 
@@ -19,49 +20,68 @@
 namespace {
 
 constexpr uint32_t kDefaultBlock = 65536;
+// Largest block: the kernels count a block's bits in u32 (payload bits,
+// sidecar bit positions, suffix sums), and block_size * 15 + header must stay
+// below 2^32 bits.
+constexpr uint32_t kMaxBlock = 1u << 28;
 
 uint64_t round_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
-// Per-(device, stream, purpose) grow-only device scratch for the two-kernel
-// encode and decode: calls on one stream are ordered, so they may share it;
-// calls on different streams get different buffers.
-struct Scratch {
+// Per-(device, stream) grow-only device workspace for the two-kernel encode
+// and decode.  A caller holds the workspace's lock (a Lease) from taking the
+// buffers until its last launch on them is enqueued: calls on one stream then
+// use the buffers in stream order, and a call that has to grow a buffer
+// synchronises the stream (the work of earlier holders has been enqueued on
+// it) before freeing the old one.  Different streams get different
+// workspaces.
+enum { SCRATCH_DT = 0, SCRATCH_DTINFO = 1, SCRATCH_BITS = 2, SCRATCH_KINDS = 3 };
+struct Workspace {
     int dev;
     void* stream;
-    int tag;
-    void* ptr;
-    uint64_t bytes;
+    std::mutex mu;
+    void* ptr[SCRATCH_KINDS] = {};
+    uint64_t bytes[SCRATCH_KINDS] = {};
 };
 std::mutex g_ws_mu;
-std::vector<Scratch> g_ws;
+std::vector<std::unique_ptr<Workspace>> g_ws;
 
-void* scratch(void* stream, int tag, uint64_t bytes) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    std::lock_guard<std::mutex> lk(g_ws_mu);
-    Scratch* w = nullptr;
-    for (auto& x : g_ws)
-        if (x.dev == dev && x.stream == stream && x.tag == tag) w = &x;
-    if (!w) {
-        g_ws.push_back(Scratch{dev, stream, tag, nullptr, 0});
-        w = &g_ws.back();
-    }
-    if (w->bytes < bytes) {
-        if (w->ptr) {
-            (void)hipStreamSynchronize(static_cast<hipStream_t>(stream));
-            (void)hipFree(w->ptr);
-            w->ptr = nullptr;
+struct Lease {
+    Workspace* ws = nullptr;
+    std::unique_lock<std::mutex> lk;
+    explicit Lease(void* stream) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess) return;
+        {
+            std::lock_guard<std::mutex> g(g_ws_mu);
+            for (auto& x : g_ws)
+                if (x->dev == dev && x->stream == stream) ws = x.get();
+            if (!ws) {
+                g_ws.push_back(std::make_unique<Workspace>());
+                ws = g_ws.back().get();
+                ws->dev = dev;
+                ws->stream = stream;
+            }
         }
-        if (hipMalloc(&w->ptr, bytes) != hipSuccess) {
-            w->bytes = 0;
-            w->ptr = nullptr;
-            return nullptr;
-        }
-        w->bytes = bytes;
+        lk = std::unique_lock<std::mutex>(ws->mu);
     }
-    return w->ptr;
-}
-enum { SCRATCH_DT = 1, SCRATCH_DTINFO = 2, SCRATCH_ENC = 3 };
+    void* get(int tag, uint64_t bytes) {
+        if (!ws) return nullptr;
+        if (ws->bytes[tag] < bytes) {
+            if (ws->ptr[tag]) {
+                (void)hipStreamSynchronize(static_cast<hipStream_t>(ws->stream));
+                (void)hipFree(ws->ptr[tag]);
+                ws->ptr[tag] = nullptr;
+            }
+            ws->bytes[tag] = 0;
+            if (hipMalloc(&ws->ptr[tag], bytes) != hipSuccess) {
+                ws->ptr[tag] = nullptr;
+                return nullptr;
+            }
+            ws->bytes[tag] = bytes;
+        }
+        return ws->ptr[tag];
+    }
+};
 
 // Tuning / ablation knobs (not part of the ABI): FSEHIP_ENC_LANES=32|64,
 // FSEHIP_DEBUG bit mask (see fse_kernels.h).
@@ -148,20 +168,29 @@ uint32_t lmax_for(const fsehip_params* p) {
     return p->table_log < 11 ? 11 : p->table_log;
 }
 
+// Kernel table bound for a max_table_log: tables are instantiated at 11
+// (L <= 11), 12 and 15 (L 13..15; normalize clamps requests to 15,
+// histogram.rs:96); 0 = 12.  Decode tables use this stride.
+uint32_t kern_lmax(uint32_t max_table_log) {
+    if (max_table_log == 0) return 12;
+    return max_table_log <= 11 ? 11 : max_table_log <= 12 ? 12 : 15;
+}
+
 // Device staging for the host-pointer entry points (grow-only, per thread).
 struct Staging {
-    uint8_t* buf[4] = {nullptr, nullptr, nullptr, nullptr};
-    size_t cap[4] = {0, 0, 0, 0};
+    static constexpr int K = 8;
+    uint8_t* buf[K] = {};
+    size_t cap[K] = {};
     int device = -1;
     ~Staging() {
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < K; ++i)
             if (buf[i]) (void)hipFree(buf[i]);
     }
     uint8_t* get(int i, size_t bytes) {
         int dev = 0;
         (void)hipGetDevice(&dev);
         if (dev != device) {
-            for (int j = 0; j < 4; ++j) {
+            for (int j = 0; j < K; ++j) {
                 if (buf[j]) (void)hipFree(buf[j]);
                 buf[j] = nullptr;
                 cap[j] = 0;
@@ -194,8 +223,8 @@ int compress_one(const uint8_t* src, size_t n, uint32_t table_log, uint8_t* dst,
                  uint64_t* payload_bits, uint32_t nstates = 2) {
     if (!dst_len) return FSE_ERR_BAD_ARG;
     if (n == 0) return FSE_ERR_EMPTY;  // size.ilog2() panics (histogram.rs:266)
-    if (n > (1u << 28)) return FSE_ERR_UNSUPPORTED;
-    if (table_log > 12) return FSE_ERR_UNSUPPORTED;
+    if (n > kMaxBlock) return FSE_ERR_UNSUPPORTED;
+    if (table_log > 15) table_log = 15;  // Histogram::normalize clamps (histogram.rs:96)
     if (!device_ok()) return FSE_ERR_NO_DEVICE;
     fsehip_params p{(uint32_t)round_up(n, 16), table_log, 0, table_log ? std::max<uint32_t>(table_log, 11) : 11,
                     nstates};
@@ -255,12 +284,11 @@ int fsehip_compress_blocks(const fsehip_params* p, const uint8_t* d_src, uint64_
     if (!p || !d_src || !d_out || !d_comp_len || !d_status) return FSE_ERR_BAD_ARG;
     if (n_total == 0) return FSE_ERR_EMPTY;
     const uint32_t bs = p->block_size ? p->block_size : kDefaultBlock;
+    if (bs > kMaxBlock) return FSE_ERR_UNSUPPORTED;
     const uint64_t n_blocks = (n_total + bs - 1) / bs;
     if (n_blocks > 1 && (bs & 15u)) return FSE_ERR_BAD_ARG;
     if (n_blocks > 0xFFFFFFFFull) return FSE_ERR_BAD_ARG;
-    if (p->table_log > 15) return FSE_ERR_TABLELOG_RANGE;
-    const uint32_t lmax = lmax_for(p);
-    if (lmax > 12) return FSE_ERR_UNSUPPORTED;
+    const uint32_t lmax = kern_lmax(lmax_for(p));
     if (slot_bytes & 15u) return FSE_ERR_BAD_ARG;
     const uint32_t ns = p->nstates == 1 ? 1u : 2u;
     if (p->nstates > 2) return FSE_ERR_BAD_ARG;
@@ -284,27 +312,7 @@ int fsehip_compress_blocks(const fsehip_params* p, const uint8_t* d_src, uint64_
     P.status = d_status;
     P.lanes = (ns == 2 && env_u32("FSEHIP_ENC_LANES", 64) == 32) ? 32 : 64;
     P.debug = env_u32("FSEHIP_DEBUG", 0);
-    // scratch-path lane streams: worst case of a lane's steps at L = lmax,
-    // plus the top lane's extra step and lane 0's finals + marker, in whole
-    // 128-byte lines so no two lanes share a cache line
-    // (measured slower than the repair path on C2, skewed and uniform data:
-    // opt-in, FSEHIP_ENC_PATH=2 or 0 = by distribution)
-    P.path = env_u32("FSEHIP_ENC_PATH", 1);
-    P.warm = env_u32("FSEHIP_ENC_WARM", 64);
-    P.pmax256 = env_u32("FSEHIP_ENC_PMAX", 128);
-    P.xlds = env_u32("FSEHIP_ENC_XLDS", 0);
-    P.scratch = nullptr;
-    if (P.path != 1 && P.lanes == 64 && ns == 2) {
-        const uint64_t steps = ns == 2 ? (bs >= 2 ? bs / 2 - 1 : 1) : (bs >= 1 ? bs - 1 : 1);
-        const uint64_t spc = ns == 2 ? 8 : 16;
-        uint64_t S = (steps + P.lanes - 1) / P.lanes;
-        S = std::max<uint64_t>(spc, (S + spc - 1) / spc * spc);
-        const uint64_t maxbits = S * ns * lmax + 3ull * lmax + 1;
-        P.scr_lane_words = (uint32_t)round_up((maxbits + 31) / 32 + 1, 32);
-        P.scratch = static_cast<uint32_t*>(
-            scratch(stream, SCRATCH_ENC, n_blocks * P.lanes * (uint64_t)P.scr_lane_words * 4u));
-        if (!P.scratch) return FSE_ERR_HIP;
-    }
+    P.xlds = env_u32("FSEHIP_ENC_XLDS", 0);  // diagnostics: occupancy probe
     const size_t groups = (n_blocks * P.lanes + 63) / 64;
     P.stamps = g_stamps_enc.get(groups);
     hipError_t e = fsehip::launch_encode(P, lmax, static_cast<hipStream_t>(stream));
@@ -312,22 +320,26 @@ int fsehip_compress_blocks(const fsehip_params* p, const uint8_t* d_src, uint64_
     return e == hipSuccess ? FSE_OK : FSE_ERR_HIP;
 }
 
+// Decode on prebuilt tables (dtable_blocks_kernel at stride kern_lmax):
+// segment-parallel with a sidecar, else serial (container mode when n_total
+// is known, the reference's own termination within out_cap otherwise).
 static int decompress_impl(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
                            const uint32_t* d_comp_len, const uint64_t* d_sidecar, uint8_t* d_out, uint64_t n_total,
                            uint64_t* d_sidecar_out, int32_t* d_status, uint32_t* d_out_len, uint32_t out_cap,
-                           fsehip_stream_t stream, const uint32_t* d_dt = nullptr,
-                           const int32_t* d_dtinfo = nullptr) {
-    if (!p || !d_in || !d_comp_len || !d_out || !d_status) return FSE_ERR_BAD_ARG;
+                           fsehip_stream_t stream, const uint32_t* d_dt, const int32_t* d_dtinfo) {
+    if (!p || !d_in || !d_comp_len || !d_out || !d_status || !d_dt || !d_dtinfo) return FSE_ERR_BAD_ARG;
     const uint32_t bs = p->block_size ? p->block_size : kDefaultBlock;
+    if (bs > kMaxBlock) return FSE_ERR_UNSUPPORTED;
     const uint64_t n_blocks = n_total ? (n_total + bs - 1) / bs : 1;
     if (n_blocks > 1 && (bs & 15u)) return FSE_ERR_BAD_ARG;
+    if (n_blocks > 0xFFFFFFFFull) return FSE_ERR_BAD_ARG;
     if (slot_bytes & 3u) return FSE_ERR_BAD_ARG;
     const uint32_t ns = p->nstates == 1 ? 1u : 2u;
     if (p->nstates > 2) return FSE_ERR_BAD_ARG;
     if ((d_sidecar || d_sidecar_out) &&
         (p->ckpt_interval < (ns == 1 ? 16u : 8u) || (p->ckpt_interval & (p->ckpt_interval - 1))))
         return FSE_ERR_BAD_ARG;
-    if (ns == 1 && (!d_dt || d_sidecar_out)) return FSE_ERR_UNSUPPORTED;  // 1-state runs on prebuilt tables only
+    if (ns == 1 && d_sidecar_out) return FSE_ERR_UNSUPPORTED;  // the recorder is the 2-state serial decoder
     if (!device_ok()) return FSE_ERR_NO_DEVICE;
     fsehip::DecParams P{};
     P.nstates = ns;
@@ -345,26 +357,15 @@ static int decompress_impl(const fsehip_params* p, const uint8_t* d_in, uint64_t
     P.status = d_status;
     P.out_len = d_out_len;
     P.sidecar_out = d_sidecar_out;
-    P.debug = env_u32("FSEHIP_DEBUG", 0) >> 4;
-    P.waves = env_u32("FSEHIP_DEC_WAVES", 4) == 8 ? 8 : 4;
-    P.variant = env_u32("FSEHIP_DEC_VAR", 12);
-    P.dual = env_u32("FSEHIP_DEC_DUAL", 0);
-    P.stage_kib = env_u32("FSEHIP_DEC_PP", 44);
-    // the decoder reads L from each header; size its tables for the bound
-    uint32_t lmax = p->max_table_log ? p->max_table_log : 12;
     P.dt = d_dt;
     P.dtinfo = d_dtinfo;
     P.stamps = g_stamps_dec.get(n_blocks);
-    hipError_t e = fsehip::launch_decode(P, lmax, static_cast<hipStream_t>(stream));
+    hipError_t e = fsehip::launch_decode(P, kern_lmax(p->max_table_log), static_cast<hipStream_t>(stream));
     if (P.stamps) g_stamps_dec.report("decode", n_blocks, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? FSE_OK : FSE_ERR_HIP;
 }
 
-static uint32_t dt_lmax(const fsehip_params* p) { return (p && p->max_table_log && p->max_table_log <= 11) ? 11 : 12; }
-
-uint64_t fsehip_dtable_bytes(uint32_t max_table_log) {
-    return 4ull << ((max_table_log && max_table_log <= 11) ? 11 : 12);
-}
+uint64_t fsehip_dtable_bytes(uint32_t max_table_log) { return 4ull << kern_lmax(max_table_log); }
 
 int fsehip_build_dtables(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes, const uint32_t* d_comp_len,
                          uint32_t n_blocks, uint32_t* d_dtables, int32_t* d_dtinfo, fsehip_stream_t stream) {
@@ -372,14 +373,13 @@ int fsehip_build_dtables(const fsehip_params* p, const uint8_t* d_in, uint64_t s
     if (n_blocks == 0) return FSE_OK;
     if (!device_ok()) return FSE_ERR_NO_DEVICE;
     fsehip::DtParams D{};
-    D.debug = env_u32("FSEHIP_DT_DEBUG", 0);
     D.in = d_in;
     D.slot_bytes = slot_bytes;
     D.comp_len = d_comp_len;
     D.n_blocks = n_blocks;
     D.dt = d_dtables;
     D.dtinfo = d_dtinfo;
-    hipError_t e = fsehip::launch_dtables(D, dt_lmax(p), static_cast<hipStream_t>(stream));
+    hipError_t e = fsehip::launch_dtables(D, kern_lmax(p->max_table_log), static_cast<hipStream_t>(stream));
     return e == hipSuccess ? FSE_OK : FSE_ERR_HIP;
 }
 
@@ -390,61 +390,54 @@ int fsehip_decompress_blocks_dt(const fsehip_params* p, const uint8_t* d_in, uin
     if (n_total == 0) return FSE_ERR_EMPTY;
     if (!p || !d_dtables || !d_dtinfo) return FSE_ERR_BAD_ARG;
     if (d_sidecar && p->ckpt_interval == 0) return FSE_ERR_BAD_ARG;
-    // without a sidecar: 2-state blocks take the speculative sync decoder,
-    // 1-state blocks the serial one
-    fsehip_params q = *p;
-    q.max_table_log = dt_lmax(p);  // the table stride the tables were built with
-    return decompress_impl(&q, d_in, slot_bytes, d_comp_len, d_sidecar, d_out, n_total, nullptr, d_status, nullptr,
-                           0, stream, d_dtables, d_dtinfo);
+    return decompress_impl(p, d_in, slot_bytes, d_comp_len, d_sidecar, d_out, n_total, nullptr, d_status, nullptr, 0,
+                           stream, d_dtables, d_dtinfo);
 }
 
+extern "C++" {
+// Decode tables for all blocks at high occupancy into the stream's
+// workspace, then `run(dt, info)` enqueues the decode on them; both under
+// the workspace lock.
+template <class Run>
+static int with_dtables(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes, const uint32_t* d_comp_len,
+                        uint64_t n_total, fsehip_stream_t stream, Run run) {
+    const uint32_t bs = p->block_size ? p->block_size : kDefaultBlock;
+    if (bs > kMaxBlock) return FSE_ERR_UNSUPPORTED;
+    const uint64_t n_blocks = (n_total + bs - 1) / bs;
+    if (n_blocks > 0xFFFFFFFFull) return FSE_ERR_BAD_ARG;
+    if (!device_ok()) return FSE_ERR_NO_DEVICE;
+    Lease lease(stream);
+    uint32_t* dt = static_cast<uint32_t*>(lease.get(SCRATCH_DT, fsehip_dtable_bytes(p->max_table_log) * n_blocks));
+    int32_t* info = static_cast<int32_t*>(lease.get(SCRATCH_DTINFO, 4ull * n_blocks));
+    if (!dt || !info) return FSE_ERR_HIP;
+    int rc = fsehip_build_dtables(p, d_in, slot_bytes, d_comp_len, (uint32_t)n_blocks, dt, info, stream);
+    return rc != FSE_OK ? rc : run(dt, info);
+}
+}  // extern "C++"
 
 int fsehip_decompress_blocks(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
                              const uint32_t* d_comp_len, const uint64_t* d_sidecar, uint8_t* d_out, uint64_t n_total,
                              int32_t* d_status, fsehip_stream_t stream) {
     if (n_total == 0) return FSE_ERR_EMPTY;
-    if (d_sidecar && p && p->ckpt_interval == 0) return FSE_ERR_BAD_ARG;
-    // FSEHIP_DEC_FUSED=1: the one-kernel path (serial one lane per block without a sidecar)
-    if (p && (p->nstates == 1 || !env_u32("FSEHIP_DEC_FUSED", 0))) {
-        // two kernels: decode tables for all blocks at high occupancy, then
-        // the LDS-heavy segment decode with no serial phase
-        const uint32_t bs = p->block_size ? p->block_size : kDefaultBlock;
-        const uint64_t n_blocks = (n_total + bs - 1) / bs;
-        if (!device_ok()) return FSE_ERR_NO_DEVICE;
-        uint32_t* dt = static_cast<uint32_t*>(scratch(stream, SCRATCH_DT, fsehip_dtable_bytes(p->max_table_log) * n_blocks));
-        int32_t* info = static_cast<int32_t*>(scratch(stream, SCRATCH_DTINFO, 4ull * n_blocks));
-        if (!dt || !info) return FSE_ERR_HIP;
-        int rc = fsehip_build_dtables(p, d_in, slot_bytes, d_comp_len, (uint32_t)n_blocks, dt, info, stream);
-        if (rc != FSE_OK) return rc;
+    if (!p) return FSE_ERR_BAD_ARG;
+    if (d_sidecar && p->ckpt_interval == 0) return FSE_ERR_BAD_ARG;
+    return with_dtables(p, d_in, slot_bytes, d_comp_len, n_total, stream, [&](const uint32_t* dt, const int32_t* info) {
         return fsehip_decompress_blocks_dt(p, d_in, slot_bytes, d_comp_len, d_sidecar, dt, info, d_out, n_total,
                                            d_status, stream);
-    }
-    return decompress_impl(p, d_in, slot_bytes, d_comp_len, d_sidecar, d_out, n_total, nullptr, d_status, nullptr,
-                           0, stream);
+    });
 }
 
 int fsehip_build_sidecar(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
                          const uint32_t* d_comp_len, uint8_t* d_out, uint64_t n_total, uint64_t* d_sidecar_out,
                          int32_t* d_status, fsehip_stream_t stream) {
     if (n_total == 0) return FSE_ERR_EMPTY;
-    if (p && p->nstates != 1 && d_sidecar_out && !env_u32("FSEHIP_DEC_FUSED", 0)) {
-        // tables for all blocks, then the serial decoder (table in LDS, 20 blocks per CU) records it
-        if (p->ckpt_interval < 8 || (p->ckpt_interval & (p->ckpt_interval - 1))) return FSE_ERR_BAD_ARG;
-        const uint32_t bs = p->block_size ? p->block_size : kDefaultBlock;
-        const uint64_t n_blocks = (n_total + bs - 1) / bs;
-        if (!device_ok()) return FSE_ERR_NO_DEVICE;
-        uint32_t* dt = static_cast<uint32_t*>(scratch(stream, SCRATCH_DT, fsehip_dtable_bytes(p->max_table_log) * n_blocks));
-        int32_t* info = static_cast<int32_t*>(scratch(stream, SCRATCH_DTINFO, 4ull * n_blocks));
-        if (!dt || !info) return FSE_ERR_HIP;
-        int rc = fsehip_build_dtables(p, d_in, slot_bytes, d_comp_len, (uint32_t)n_blocks, dt, info, stream);
-        if (rc != FSE_OK) return rc;
-        fsehip_params q = *p;
-        q.max_table_log = dt_lmax(p);
-        return decompress_impl(&q, d_in, slot_bytes, d_comp_len, nullptr, d_out, n_total, d_sidecar_out, d_status,
+    if (!p || !d_sidecar_out) return FSE_ERR_BAD_ARG;
+    if (p->nstates == 1) return FSE_ERR_UNSUPPORTED;
+    if (p->ckpt_interval < 8 || (p->ckpt_interval & (p->ckpt_interval - 1))) return FSE_ERR_BAD_ARG;
+    return with_dtables(p, d_in, slot_bytes, d_comp_len, n_total, stream, [&](const uint32_t* dt, const int32_t* info) {
+        return decompress_impl(p, d_in, slot_bytes, d_comp_len, nullptr, d_out, n_total, d_sidecar_out, d_status,
                                nullptr, 0, stream, dt, info);
-    }
-    return decompress_impl(p, d_in, slot_bytes, d_comp_len, nullptr, d_out, n_total, d_sidecar_out, d_status,
-                           nullptr, 0, stream);
+    });
 }
 
 int fsehip_histogram_blocks(const uint8_t* d_src, uint64_t n_total, uint32_t block_size, uint32_t* d_counts,
@@ -529,45 +522,16 @@ int fse_compress2(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, si
 
 int fse_compress2_log(const uint8_t* src, size_t n, uint32_t table_log, uint8_t* dst, size_t dst_cap,
                       size_t* dst_len, uint64_t* payload_bits) {
-    if (table_log == 0) return FSE_ERR_TABLELOG_RANGE;
-    return compress_one(src, n, table_log, dst, dst_cap, dst_len, payload_bits);
+    // Histogram::normalize clamps any request into 5..15 (histogram.rs:96):
+    // 0 acts as 5 (table_log 0 in the batched params means NormHistogram::new)
+    return compress_one(src, n, std::max<uint32_t>(table_log, 5u), dst, dst_cap, dst_len, payload_bits);
 }
 
-int fse_decompress2(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, size_t* dst_len) {
-    if (!dst_len || *dst_len > dst_cap) return FSE_ERR_BAD_ARG;
-    if (n == 0) return FSE_ERR_EMPTY;  // BitStreamReader::new asserts (stream_reader.rs:17)
-    if (n > (1u << 30)) return FSE_ERR_UNSUPPORTED;
-    if (!device_ok()) return FSE_ERR_NO_DEVICE;
-    const uint64_t padded = round_up(n, 16) + 16;
-    const uint64_t cap64 = std::min<uint64_t>(dst_cap - *dst_len, 0x7FFFFFFFu);
-    uint8_t* d_in = g_stage.get(0, padded);
-    uint8_t* d_out = g_stage.get(1, std::max<uint64_t>(cap64, 16));
-    uint8_t* d_meta = g_stage.get(2, sizeof(Meta));
-    if (!d_in || !d_out || !d_meta) return FSE_ERR_HIP;
-    if (hipMemset(d_in, 0, padded) != hipSuccess) return FSE_ERR_HIP;
-    if (hipMemcpy(d_in, src, n, hipMemcpyHostToDevice) != hipSuccess) return FSE_ERR_HIP;
-    Meta* m = reinterpret_cast<Meta*>(d_meta);
-    Meta h0{(uint32_t)n, 0, 0, 0};
-    if (hipMemcpy(d_meta, &h0, sizeof(Meta), hipMemcpyHostToDevice) != hipSuccess) return FSE_ERR_HIP;
-    fsehip_params p{0, 0, 0, 12};
-    int rc = decompress_impl(&p, d_in, padded, &m->comp_len, nullptr, d_out, 0, nullptr, &m->status,
-                             &m->payload_bits, (uint32_t)cap64, nullptr);
-    if (rc) return rc;
-    Meta h{};
-    if (hipMemcpy(&h, d_meta, sizeof(Meta), hipMemcpyDeviceToHost) != hipSuccess) return FSE_ERR_HIP;
-    if (h.status != FSE_OK) return h.status;
-    const uint32_t out_len = h.payload_bits;  // decoded byte count
-    if (out_len && hipMemcpy(dst + *dst_len, d_out, out_len, hipMemcpyDeviceToHost) != hipSuccess) return FSE_ERR_HIP;
-    *dst_len += out_len;
-    return FSE_OK;
-}
-
-int fse_compress(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, size_t* dst_len, uint64_t* payload_bits) {
-    // lib.rs:112-143; n == 1 is valid here (a lone seed state), unlike fse_compress2
-    return compress_one(src, n, 0, dst, dst_cap, dst_len, payload_bits, 1);
-}
-
-int fse_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, size_t* dst_len) {
+// Host block decode (reference mode: the raw length is not in the format):
+// the block's table (stride 15, any L) and the serial decoder with the
+// reference's own termination within the caller's capacity.
+static int decompress_one(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, size_t* dst_len,
+                          uint32_t nstates) {
     if (!dst_len || *dst_len > dst_cap) return FSE_ERR_BAD_ARG;
     if (n == 0) return FSE_ERR_EMPTY;  // BitStreamReader::new asserts (stream_reader.rs:17)
     if (n > (1u << 30)) return FSE_ERR_UNSUPPORTED;
@@ -577,16 +541,16 @@ int fse_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, s
     uint8_t* d_in = g_stage.get(0, padded);
     uint8_t* d_out = g_stage.get(1, std::max<uint64_t>(cap64, 16));
     uint8_t* d_meta = g_stage.get(2, sizeof(Meta));
-    uint8_t* d_dt = g_stage.get(3, fsehip_dtable_bytes(12) + 16);
+    uint8_t* d_dt = g_stage.get(3, fsehip_dtable_bytes(15) + 16);
     if (!d_in || !d_out || !d_meta || !d_dt) return FSE_ERR_HIP;
     if (hipMemset(d_in, 0, padded) != hipSuccess) return FSE_ERR_HIP;
     if (hipMemcpy(d_in, src, n, hipMemcpyHostToDevice) != hipSuccess) return FSE_ERR_HIP;
     Meta* m = reinterpret_cast<Meta*>(d_meta);
     Meta h0{(uint32_t)n, 0, 0, 0};
     if (hipMemcpy(d_meta, &h0, sizeof(Meta), hipMemcpyHostToDevice) != hipSuccess) return FSE_ERR_HIP;
-    fsehip_params p{0, 0, 0, 12, 1};
+    fsehip_params p{0, 0, 0, 15, nstates};
     uint32_t* dt = reinterpret_cast<uint32_t*>(d_dt);
-    int32_t* info = reinterpret_cast<int32_t*>(d_dt + fsehip_dtable_bytes(12));
+    int32_t* info = reinterpret_cast<int32_t*>(d_dt + fsehip_dtable_bytes(15));
     int rc = fsehip_build_dtables(&p, d_in, padded, &m->comp_len, 1, dt, info, nullptr);
     if (rc) return rc;
     rc = decompress_impl(&p, d_in, padded, &m->comp_len, nullptr, d_out, 0, nullptr, &m->status, &m->payload_bits,
@@ -599,6 +563,19 @@ int fse_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, s
     if (out_len && hipMemcpy(dst + *dst_len, d_out, out_len, hipMemcpyDeviceToHost) != hipSuccess) return FSE_ERR_HIP;
     *dst_len += out_len;
     return FSE_OK;
+}
+
+int fse_decompress2(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, size_t* dst_len) {
+    return decompress_one(src, n, dst, dst_cap, dst_len, 2);
+}
+
+int fse_compress(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, size_t* dst_len, uint64_t* payload_bits) {
+    // lib.rs:112-143; n == 1 is valid here (a lone seed state), unlike fse_compress2
+    return compress_one(src, n, 0, dst, dst_cap, dst_len, payload_bits, 1);
+}
+
+int fse_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, size_t* dst_len) {
+    return decompress_one(src, n, dst, dst_cap, dst_len, 1);
 }
 
 int histogram_count(const uint8_t* src, size_t n, uint32_t counts[256], uint32_t* table_len) {
@@ -616,6 +593,287 @@ int histogram_count(const uint8_t* src, size_t n, uint32_t counts[256], uint32_t
     if (hipMemcpy(h, d_cnt, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess) return FSE_ERR_HIP;
     memcpy(counts, h, 256 * sizeof(uint32_t));
     if (table_len) *table_len = h[256];
+    return FSE_OK;
+}
+
+// ------------------------------------------------------- building blocks
+
+int histogram_new(const uint8_t* src, size_t n, fse_histogram* out) {
+    if (!out) return FSE_ERR_BAD_ARG;
+    uint32_t tl = 0;
+    int rc = histogram_count(src, n, out->counts, &tl);
+    if (rc) return rc;
+    out->size = (uint32_t)n;
+    out->table_len = tl;
+    return FSE_OK;
+}
+
+// One normalisation on the GPU (fse_blocks.hip norm_kernel).
+static int normalize_dev(int mode, const uint8_t* src, size_t n, const fse_histogram* h, uint32_t log2,
+                         fse_norm_histogram* out) {
+    if (!out) return FSE_ERR_BAD_ARG;
+    if (mode == 2 && n > 0xFFFFFFFFull) return FSE_ERR_BAD_ARG;  // histogram.rs:19 assert
+    if (!device_ok()) return FSE_ERR_NO_DEVICE;
+    uint8_t* d_src = mode == 2 ? g_stage.get(0, round_up(n, 16) + 16) : nullptr;
+    uint8_t* d_io = g_stage.get(2, sizeof(fse_norm_histogram) + sizeof(fse_histogram) + 16);
+    if ((mode == 2 && !d_src) || !d_io) return FSE_ERR_HIP;
+    auto* d_nh = reinterpret_cast<fse_norm_histogram*>(d_io);
+    auto* d_h = reinterpret_cast<fse_histogram*>(d_io + sizeof(fse_norm_histogram));
+    int32_t* d_st = reinterpret_cast<int32_t*>(d_io + sizeof(fse_norm_histogram) + sizeof(fse_histogram));
+    if (mode == 2 && n && hipMemcpy(d_src, src, n, hipMemcpyHostToDevice) != hipSuccess) return FSE_ERR_HIP;
+    if (mode != 2 && hipMemcpy(d_h, h, sizeof(fse_histogram), hipMemcpyHostToDevice) != hipSuccess) return FSE_ERR_HIP;
+    fsehip::NormArgs A{};
+    A.mode = mode;
+    A.src = d_src;
+    A.n = n;
+    A.counts = d_h->counts;
+    if (mode != 2) {
+        A.size = h->size;
+        A.table_len = h->table_len;
+    }
+    A.log2 = log2;
+    A.out = d_nh;
+    A.status = d_st;
+    if (fsehip::launch_norm(A, nullptr) != hipSuccess) return FSE_ERR_HIP;
+    int32_t st = 0;
+    if (hipMemcpy(&st, d_st, 4, hipMemcpyDeviceToHost) != hipSuccess) return FSE_ERR_HIP;
+    if (st != FSE_OK) return st;
+    if (hipMemcpy(out, d_nh, sizeof(fse_norm_histogram), hipMemcpyDeviceToHost) != hipSuccess) return FSE_ERR_HIP;
+    return FSE_OK;
+}
+
+int histogram_normalize(const fse_histogram* h, uint32_t log2, fse_norm_histogram* out) {
+    if (!h || h->table_len > 256) return FSE_ERR_BAD_ARG;
+    return normalize_dev(0, nullptr, 0, h, log2, out);
+}
+
+int histogram_normalize_optimal(const fse_histogram* h, fse_norm_histogram* out) {
+    if (!h || h->table_len > 256) return FSE_ERR_BAD_ARG;
+    return normalize_dev(1, nullptr, 0, h, 0, out);
+}
+
+int norm_histogram_new(const uint8_t* src, size_t n, fse_norm_histogram* out) {
+    if (!src && n) return FSE_ERR_BAD_ARG;
+    return normalize_dev(2, src, n, nullptr, 0, out);
+}
+
+int norm_histogram_write(const fse_norm_histogram* nh, uint8_t* dst, size_t dst_cap, size_t* dst_len,
+                         uint64_t* bits_written) {
+    if (!nh || !dst_len || *dst_len > dst_cap) return FSE_ERR_BAD_ARG;
+    if (!device_ok()) return FSE_ERR_NO_DEVICE;
+    uint8_t* d = g_stage.get(2, sizeof(fse_norm_histogram) + 16 + 512);
+    if (!d) return FSE_ERR_HIP;
+    auto* d_nh = reinterpret_cast<fse_norm_histogram*>(d);
+    uint32_t* d_meta = reinterpret_cast<uint32_t*>(d + sizeof(fse_norm_histogram));  // bits, status
+    uint8_t* d_out = d + sizeof(fse_norm_histogram) + 16;
+    if (hipMemcpy(d_nh, nh, sizeof(*nh), hipMemcpyHostToDevice) != hipSuccess) return FSE_ERR_HIP;
+    if (fsehip::launch_hdr_write(d_nh, d_out, d_meta, reinterpret_cast<int32_t*>(d_meta + 1), nullptr) != hipSuccess)
+        return FSE_ERR_HIP;
+    uint32_t meta[2];
+    if (hipMemcpy(meta, d_meta, 8, hipMemcpyDeviceToHost) != hipSuccess) return FSE_ERR_HIP;
+    if ((int32_t)meta[1] != FSE_OK) return (int32_t)meta[1];
+    const size_t len = (meta[0] + 7u) / 8u;
+    if (dst_cap - *dst_len < len) return FSE_ERR_DST_TOO_SMALL;
+    if (len && (!dst || hipMemcpy(dst + *dst_len, d_out, len, hipMemcpyDeviceToHost) != hipSuccess))
+        return FSE_ERR_HIP;
+    *dst_len += len;
+    if (bits_written) *bits_written = meta[0];
+    return FSE_OK;
+}
+
+int norm_histogram_read(const uint8_t* src, size_t n, fse_norm_histogram* out, size_t* consumed) {
+    if (!out || (!src && n)) return FSE_ERR_BAD_ARG;
+    if (n == 0) return FSE_ERR_EMPTY;  // BitStreamReader::new asserts a non-empty slice (stream_reader.rs:17)
+    if (!device_ok()) return FSE_ERR_NO_DEVICE;
+    const size_t take = std::min<size_t>(n, 512);  // a header never exceeds 483 bytes (write_bound)
+    uint8_t* d = g_stage.get(2, sizeof(fse_norm_histogram) + 16 + 528);
+    if (!d) return FSE_ERR_HIP;
+    auto* d_nh = reinterpret_cast<fse_norm_histogram*>(d);
+    uint32_t* d_meta = reinterpret_cast<uint32_t*>(d + sizeof(fse_norm_histogram));  // used, status
+    uint8_t* d_in = d + sizeof(fse_norm_histogram) + 16;
+    if (hipMemset(d_in, 0, 528) != hipSuccess || hipMemcpy(d_in, src, take, hipMemcpyHostToDevice) != hipSuccess)
+        return FSE_ERR_HIP;
+    // the reader sees the whole slice's length (its bounds checks), the
+    // header's bits come from the first 512 bytes
+    if (fsehip::launch_hdr_read(d_in, (uint32_t)std::min<size_t>(n, 0xFFFFFFFFu), d_nh, d_meta,
+                                reinterpret_cast<int32_t*>(d_meta + 1), nullptr) != hipSuccess)
+        return FSE_ERR_HIP;
+    uint32_t meta[2];
+    if (hipMemcpy(meta, d_meta, 8, hipMemcpyDeviceToHost) != hipSuccess) return FSE_ERR_HIP;
+    if ((int32_t)meta[1] != FSE_OK) return (int32_t)meta[1];
+    if (hipMemcpy(out, d_nh, sizeof(*out), hipMemcpyDeviceToHost) != hipSuccess) return FSE_ERR_HIP;
+    if (consumed) *consumed = meta[0];
+    return FSE_OK;
+}
+
+static int table_new(const fse_norm_histogram* nh, int enc, void* out, size_t bytes) {
+    if (!nh || !out) return FSE_ERR_BAD_ARG;
+    if (!device_ok()) return FSE_ERR_NO_DEVICE;
+    uint8_t* d = g_stage.get(4, sizeof(fse_norm_histogram) + 16 + bytes);
+    if (!d) return FSE_ERR_HIP;
+    auto* d_nh = reinterpret_cast<fse_norm_histogram*>(d);
+    int32_t* d_st = reinterpret_cast<int32_t*>(d + sizeof(fse_norm_histogram));
+    uint8_t* d_tab = d + sizeof(fse_norm_histogram) + 16;
+    if (hipMemcpy(d_nh, nh, sizeof(*nh), hipMemcpyHostToDevice) != hipSuccess) return FSE_ERR_HIP;
+    if (hipMemset(d_tab, 0, bytes) != hipSuccess) return FSE_ERR_HIP;
+    if (fsehip::launch_table(d_nh, enc, reinterpret_cast<fse_encode_table*>(d_tab),
+                             reinterpret_cast<fse_decode_table*>(d_tab), d_st, nullptr) != hipSuccess)
+        return FSE_ERR_HIP;
+    int32_t st = 0;
+    if (hipMemcpy(&st, d_st, 4, hipMemcpyDeviceToHost) != hipSuccess) return FSE_ERR_HIP;
+    if (st != FSE_OK) return st;
+    return hipMemcpy(out, d_tab, bytes, hipMemcpyDeviceToHost) == hipSuccess ? FSE_OK : FSE_ERR_HIP;
+}
+
+int encode_table_new(const fse_norm_histogram* nh, fse_encode_table* out) {
+    return table_new(nh, 1, out, sizeof(fse_encode_table));
+}
+
+int decode_table_new(const fse_norm_histogram* nh, fse_decode_table* out) {
+    return table_new(nh, 0, out, sizeof(fse_decode_table));
+}
+
+int fse_compress_nh(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, size_t* dst_len,
+                    uint64_t* payload_bits, fse_norm_histogram* nh) {
+    const size_t at = dst_len ? *dst_len : 0;
+    int rc = fse_compress(src, n, dst, dst_cap, dst_len, payload_bits);
+    if (rc || !nh) return rc;
+    // the returned NormHistogram is the one the block's header carries
+    return norm_histogram_read(dst + at, *dst_len - at, nh, nullptr);
+}
+
+// ------------------------------------------------------------- bitstream
+
+// Scan of the widths into the workspace of `stream`; returns the device
+// tile offsets and total (valid in stream order).
+static int bits_scan(Lease& lease, const uint8_t* d_nbits, uint64_t count, uint64_t** tile_off, uint64_t** total,
+                     fsehip_stream_t stream) {
+    const uint64_t nt = fsehip::bits_tiles(count);
+    uint8_t* w = static_cast<uint8_t*>(lease.get(SCRATCH_BITS, 16 + nt * 12 + 16));
+    if (!w) return FSE_ERR_HIP;
+    *total = reinterpret_cast<uint64_t*>(w);
+    *tile_off = reinterpret_cast<uint64_t*>(w + 16);
+    uint32_t* tile_sum = reinterpret_cast<uint32_t*>(w + 16 + nt * 8);
+    return fsehip::launch_bits_scan(d_nbits, count, tile_sum, *tile_off, *total, static_cast<hipStream_t>(stream)) ==
+                   hipSuccess
+               ? FSE_OK
+               : FSE_ERR_HIP;
+}
+
+int fsehip_bitstack_write(const uint32_t* d_vals, const uint8_t* d_nbits, uint64_t count, uint8_t* d_out,
+                          uint64_t out_cap, uint64_t* d_total_bits, fsehip_stream_t stream) {
+    if ((count && (!d_vals || !d_nbits)) || !d_out || !d_total_bits || (reinterpret_cast<uintptr_t>(d_out) & 3u))
+        return FSE_ERR_BAD_ARG;
+    if (!device_ok()) return FSE_ERR_NO_DEVICE;
+    Lease lease(stream);
+    uint64_t *tile_off = nullptr, *total = nullptr;
+    int rc = bits_scan(lease, d_nbits, count, &tile_off, &total, stream);
+    if (rc) return rc;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (fsehip::launch_bits_pack(d_vals, d_nbits, count, tile_off, total, reinterpret_cast<uint32_t*>(d_out),
+                                 out_cap / 4u, s) != hipSuccess)
+        return FSE_ERR_HIP;
+    return hipMemcpyAsync(d_total_bits, total, 8, hipMemcpyDeviceToDevice, s) == hipSuccess ? FSE_OK : FSE_ERR_HIP;
+}
+
+static int bits_read_dev(const uint8_t* d_in, uint64_t n_bytes, uint64_t total_bits, int stack, const uint8_t* d_nbits,
+                         uint64_t count, uint32_t* d_vals, uint64_t* d_result, fsehip_stream_t stream) {
+    if ((count && (!d_nbits || !d_vals)) || !d_result || (!d_in && n_bytes)) return FSE_ERR_BAD_ARG;
+    if (!device_ok()) return FSE_ERR_NO_DEVICE;
+    Lease lease(stream);
+    uint64_t *tile_off = nullptr, *total = nullptr;
+    int rc = bits_scan(lease, d_nbits, count, &tile_off, &total, stream);
+    if (rc) return rc;
+    return fsehip::launch_bits_unpack(d_in, n_bytes, total_bits, stack, d_nbits, count, tile_off, total, d_vals,
+                                      d_result, static_cast<hipStream_t>(stream)) == hipSuccess
+               ? FSE_OK
+               : FSE_ERR_HIP;
+}
+
+int fsehip_bitstack_read(const uint8_t* d_in, uint64_t n_bytes, const uint8_t* d_nbits, uint64_t count,
+                         uint32_t* d_vals, uint64_t* d_result, fsehip_stream_t stream) {
+    return bits_read_dev(d_in, n_bytes, 0, 1, d_nbits, count, d_vals, d_result, stream);
+}
+
+int fsehip_bitstream_read(const uint8_t* d_in, uint64_t n_bytes, uint64_t total_bits, const uint8_t* d_nbits,
+                          uint64_t count, uint32_t* d_vals, uint64_t* d_result, fsehip_stream_t stream) {
+    if (n_bytes == 0 || (total_bits + 7u) / 8u != n_bytes) return FSE_ERR_BAD_ARG;  // stream_reader.rs:17-21 asserts
+    return bits_read_dev(d_in, n_bytes, total_bits, 0, d_nbits, count, d_vals, d_result, stream);
+}
+
+int bitstack_write(const uint32_t* vals, const uint8_t* nbits, size_t count, uint8_t* dst, size_t dst_cap,
+                   size_t* dst_len, uint64_t* bits_written) {
+    if (!dst_len || *dst_len > dst_cap || (count && (!vals || !nbits))) return FSE_ERR_BAD_ARG;
+    if (!device_ok()) return FSE_ERR_NO_DEVICE;
+    uint8_t* d_v = g_stage.get(0, count * 4 + 16);
+    uint8_t* d_nb = g_stage.get(1, count + 16);
+    uint8_t* d_out = g_stage.get(5, count * 4 + 16);
+    uint8_t* d_tot = g_stage.get(2, 16);
+    if (!d_v || !d_nb || !d_out || !d_tot) return FSE_ERR_HIP;
+    if (count && (hipMemcpy(d_v, vals, count * 4, hipMemcpyHostToDevice) != hipSuccess ||
+                  hipMemcpy(d_nb, nbits, count, hipMemcpyHostToDevice) != hipSuccess))
+        return FSE_ERR_HIP;
+    uint64_t* tot = reinterpret_cast<uint64_t*>(d_tot);
+    int rc = fsehip_bitstack_write(reinterpret_cast<const uint32_t*>(d_v), d_nb, count, d_out, count * 4 + 16, tot,
+                                   nullptr);
+    if (rc) return rc;
+    uint64_t bits = 0;
+    if (hipMemcpy(&bits, tot, 8, hipMemcpyDeviceToHost) != hipSuccess) return FSE_ERR_HIP;
+    const size_t len = (size_t)((bits + 7u) / 8u);
+    if (dst_cap - *dst_len < len) return FSE_ERR_DST_TOO_SMALL;
+    if (len && (!dst || hipMemcpy(dst + *dst_len, d_out, len, hipMemcpyDeviceToHost) != hipSuccess))
+        return FSE_ERR_HIP;
+    *dst_len += len;
+    if (bits_written) *bits_written = bits;
+    return FSE_OK;
+}
+
+static int bits_read_host(const uint8_t* src, size_t n, uint64_t total_bits, int stack, const uint8_t* nbits,
+                          size_t count, uint32_t* vals, uint64_t res[3]) {
+    if ((count && (!nbits || !vals)) || (!src && n)) return FSE_ERR_BAD_ARG;
+    if (!device_ok()) return FSE_ERR_NO_DEVICE;
+    uint8_t* d_in = g_stage.get(0, round_up(n, 4) + 16);
+    uint8_t* d_nb = g_stage.get(1, count + 16);
+    uint8_t* d_v = g_stage.get(5, count * 4 + 16);
+    uint8_t* d_res = g_stage.get(2, 32);
+    if (!d_in || !d_nb || !d_v || !d_res) return FSE_ERR_HIP;
+    if (hipMemset(d_in, 0, round_up(n, 4) + 16) != hipSuccess) return FSE_ERR_HIP;
+    if (n && hipMemcpy(d_in, src, n, hipMemcpyHostToDevice) != hipSuccess) return FSE_ERR_HIP;
+    if (count && hipMemcpy(d_nb, nbits, count, hipMemcpyHostToDevice) != hipSuccess) return FSE_ERR_HIP;
+    uint64_t* r = reinterpret_cast<uint64_t*>(d_res);
+    int rc = stack ? fsehip_bitstack_read(d_in, n, d_nb, count, reinterpret_cast<uint32_t*>(d_v), r, nullptr)
+                   : fsehip_bitstream_read(d_in, n, total_bits, d_nb, count, reinterpret_cast<uint32_t*>(d_v), r,
+                                           nullptr);
+    if (rc) return rc;
+    if (hipMemcpy(res, r, 24, hipMemcpyDeviceToHost) != hipSuccess) return FSE_ERR_HIP;
+    if ((int64_t)res[2] != FSE_OK) return (int)(int64_t)res[2];
+    if (res[0] && hipMemcpy(vals, d_v, res[0] * 4, hipMemcpyDeviceToHost) != hipSuccess) return FSE_ERR_HIP;
+    return FSE_OK;
+}
+
+int bitstack_read(const uint8_t* src, size_t n, const uint8_t* nbits, size_t count, uint32_t* vals, size_t* n_read,
+                  int* finished) {
+    uint64_t res[3] = {0, 0, 0};
+    int rc = bits_read_host(src, n, 0, 1, nbits, count, vals, res);
+    if (rc) return rc;
+    if (n_read) *n_read = (size_t)res[0];
+    // finish() after the successful reads: all bits consumed (reads stop at
+    // the first None, which consumes nothing)
+    if (finished) *finished = res[0] == count ? (int)res[1] : 0;
+    return FSE_OK;
+}
+
+int bitstream_read(const uint8_t* src, size_t n, uint64_t total_bits, const uint8_t* nbits, size_t count,
+                   uint32_t* vals, size_t* n_read, uint64_t* bits_left) {
+    uint64_t res[3] = {0, 0, 0};
+    int rc = bits_read_host(src, n, total_bits, 0, nbits, count, vals, res);
+    if (rc) return rc;
+    if (n_read) *n_read = (size_t)res[0];
+    if (bits_left) {
+        uint64_t used = 0;
+        for (size_t i = 0; i < res[0]; ++i) used += std::min<uint32_t>(nbits[i], 32u);
+        *bits_left = total_bits - used;
+    }
     return FSE_OK;
 }
 

@@ -1,0 +1,813 @@
+// fse_decode.hip -- decode side of the batched FSE (tANS) block codec, gfx950.
+//
+// Wire format: the reference's fse_compress2 / fse_compress blocks
+// (lib.rs:112-183): NCount header || backward bit stack + marker bit.
+//
+//   dtable_blocks_kernel   NormHistogram::read + DecodeTable (histogram.rs:436-505,
+//                          fse.rs:280-338), one wave per block, table to HBM
+//   decode_pre_kernel      segment-parallel decode on prebuilt tables: one
+//                          workgroup per block, the compressed block and its
+//                          table staged in LDS, every lane decodes one
+//                          sidecar segment (checkpoint to checkpoint)
+//   serial2_decode_kernel  sidecar-less 2-state decode (container mode with
+//                          the raw length, or the reference's own termination
+//                          for host streams of unknown length), one lane per
+//                          block with its table in LDS; can record the sidecar
+//   decode1_serial_kernel  the same for 1-state blocks (fse_decompress)
+//
+// Table logs: kernels are instantiated at LMAX = 11, 12 and 15 (blocks of
+// L 5..11, 12, 13..15).  At LMAX = 15 the table (128 KiB) leaves no LDS for
+// the block image, so those blocks are read through a register window from
+// global memory.
+#include "fse_device.hpp"
+#include "fse_kernels.h"
+
+namespace fsehip {
+
+// ------------------------------------------------------------------------
+// Decode table entry (fse.rs:260-265 DecodeTransform, repacked for the
+// decode loop): nb | symbol << 8 | new_state << SH.  With SH = 18 (L <= 14)
+// the high half is the LDS byte offset of the next state's base entry
+// (4 * new_state), nb in bits 0-4 serves directly as a v_bfe width/offset
+// operand, and the byte sum of two entries' low bytes is nb0 + nb1.  L = 15
+// needs the 15-bit new_state at SH = 17 (global-window kernels only).
+// ------------------------------------------------------------------------
+template <int LMAX>
+struct Dte {
+    static constexpr uint32_t SH = LMAX > 14 ? 17u : 18u;
+    __device__ static __forceinline__ uint32_t make(uint32_t nb, uint32_t sym, uint32_t ns) {
+        return nb | (sym << 8) | (ns << SH);
+    }
+    __device__ static __forceinline__ uint32_t ns(uint32_t e) { return e >> SH; }
+};
+__device__ __forceinline__ uint32_t dte_nb(uint32_t e) { return e & 0xFFu; }
+__device__ __forceinline__ uint32_t dte_sym(uint32_t e) { return (e >> 8) & 0xFFu; }
+
+// Output group: pairs per lane between stores (32 pairs = 64 B, one HBM
+// burst).  Segment starts are multiples of ckpt_interval, so groups are 64 B
+// aligned whenever ckpt_interval >= 32.
+constexpr uint32_t DEC_GROUP = 32;
+
+// ------------------------------------------------------------------------
+// Backward bit reader over global memory (BitStackReader semantics,
+// stack_reader.rs:17-215): `pos` = bits remaining above the block start,
+// buf holds stream bits [base, base+64); refills pull the next lower word.
+// ------------------------------------------------------------------------
+struct WindowReader {
+    const uint32_t* w;
+    uint64_t buf;
+    int32_t base;
+    int32_t pos;
+    __device__ __forceinline__ void init(const uint32_t* words, int32_t p) {
+        w = words;
+        pos = p;
+        base = ((p + 31) & ~31) - 64;
+        if (base < 0) base = 0;
+        buf = (uint64_t)w[base >> 5] | ((uint64_t)w[(base >> 5) + 1] << 32);
+    }
+    __device__ __forceinline__ uint32_t pop(uint32_t nb) {
+        pos -= (int32_t)nb;
+        return (uint32_t)(buf >> (uint32_t)(pos - base)) & ((1u << nb) - 1u);
+    }
+    __device__ __forceinline__ void refill() {
+        if (pos - base < 32 && base > 0) {
+            base -= 32;
+            buf = (buf << 32) | (uint64_t)w[base >> 5];
+        }
+    }
+};
+
+// Sidecar cross-check: a segment that is not the block's last must end
+// exactly where the next checkpoint says the decoder is (bit position and
+// both states, a = 4 * state); a mismatch means the index does not belong to
+// this stream (corrupt, or built with another checkpoint interval).
+__device__ __forceinline__ bool ckpt_match(uint64_t e, int32_t hdr_bits, uint32_t smask, int32_t pos, uint32_t a0,
+                                           uint32_t a1) {
+    return (int32_t)(uint32_t)e + hdr_bits == pos && ((((uint32_t)(e >> 32) & smask) << 2) == a0) &&
+           ((((uint32_t)(e >> 48) & smask) << 2) == a1);
+}
+
+// Container-mode end of a 2-state block after its main loop (the oracle's
+// decompress2_impl with the raw length; lib.rs:227-244): the last one or two
+// symbols come from the final states, and a valid block has then read every
+// payload bit.  `ent(s)` is the table entry of state s; the reader pops.
+template <int LMAX, class Ent, class Pop>
+__device__ __forceinline__ int32_t finish2(uint32_t o, uint32_t n, uint32_t& s0, uint32_t& s1, int32_t& pos,
+                                           int32_t hdr_bits, uint8_t* __restrict__ out, Ent ent, Pop pop) {
+    for (;;) {
+        if (o + 2u == n) {
+            out[o++] = (uint8_t)dte_sym(ent(s0));
+            out[o++] = (uint8_t)dte_sym(ent(s1));
+            break;
+        }
+        if (o + 1u == n) {
+            out[o++] = (uint8_t)dte_sym(ent(s0));
+            break;
+        }
+        const uint32_t e0 = ent(s0);
+        uint32_t nb = dte_nb(e0);
+        if (pos - (int32_t)nb < hdr_bits) {
+            out[o++] = (uint8_t)dte_sym(e0);
+            if (o < n) out[o++] = (uint8_t)dte_sym(ent(s1));
+            break;
+        }
+        s0 = Dte<LMAX>::ns(e0) + pop(nb);
+        out[o++] = (uint8_t)dte_sym(e0);
+        const uint32_t e1 = ent(s1);
+        nb = dte_nb(e1);
+        if (pos - (int32_t)nb < hdr_bits) {
+            out[o++] = (uint8_t)dte_sym(e1);
+            if (o < n) out[o++] = (uint8_t)dte_sym(ent(s0));
+            break;
+        }
+        s1 = Dte<LMAX>::ns(e1) + pop(nb);
+        out[o++] = (uint8_t)dte_sym(e1);
+    }
+    return o != n ? FSE_ERR_LENGTH_MISMATCH : pos == hdr_bits ? FSE_OK : FSE_ERR_BAD_SIDECAR;
+}
+
+// Main-loop pairs [p0, p1) of one segment read through a global-memory
+// window (blocks the LDS stage cannot hold, and every block at LMAX = 15);
+// the sidecar guarantees the bits, so no read checks.  `dt` may be LDS.
+template <int LMAX>
+__device__ __forceinline__ int32_t decode_segment(WindowReader& br, uint32_t& s0, uint32_t& s1, uint32_t p0,
+                                                  uint32_t p1, bool last, uint32_t n, uint32_t Pm,
+                                                  uint8_t* __restrict__ out, const uint32_t* dt, int32_t hdr_bits) {
+    uint32_t p = p0;
+    for (; p + 8u <= p1; p += 8u) {
+        uint32_t w[4];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint32_t e0 = dt[s0], e1 = dt[s1];
+            const uint32_t v0 = br.pop(dte_nb(e0));
+            const uint32_t v1 = br.pop(dte_nb(e1));
+            s0 = Dte<LMAX>::ns(e0) + v0;
+            s1 = Dte<LMAX>::ns(e1) + v1;
+            const uint32_t pr = __builtin_amdgcn_perm(e1, e0, 0x0c0c0501u);
+            if (j & 1) w[j >> 1] |= pr << 16; else w[j >> 1] = pr;
+            br.refill();
+        }
+        *reinterpret_cast<uint4*>(out + 2u * p) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    for (; p < p1; ++p) {
+        const uint32_t e0 = dt[s0], e1 = dt[s1];
+        const uint32_t v0 = br.pop(dte_nb(e0));
+        const uint32_t v1 = br.pop(dte_nb(e1));
+        s0 = Dte<LMAX>::ns(e0) + v0;
+        s1 = Dte<LMAX>::ns(e1) + v1;
+        out[2u * p] = (uint8_t)dte_sym(e0);
+        out[2u * p + 1u] = (uint8_t)dte_sym(e1);
+        br.refill();
+    }
+    if (!last) return FSE_OK;
+    return finish2<LMAX>(2u * Pm, n, s0, s1, br.pos, hdr_bits, out, [&](uint32_t s) { return dt[s]; },
+                         [&](uint32_t nb) {
+                             const uint32_t v = br.pop(nb);
+                             br.refill();
+                             return v;
+                         });
+}
+
+// 1-state segment (fse_decompress, lib.rs:187-211) through the window.
+template <int LMAX>
+__device__ __forceinline__ int32_t decode_segment1(WindowReader& br, uint32_t& s, uint32_t p, uint32_t p1, bool last,
+                                                   uint32_t n, uint8_t* __restrict__ out, const uint32_t* dt,
+                                                   int32_t hdr_bits) {
+    for (; p < p1; ++p) {
+        const uint32_t e = dt[s];
+        s = Dte<LMAX>::ns(e) + br.pop(dte_nb(e));
+        br.refill();
+        out[p] = (uint8_t)dte_sym(e);
+    }
+    if (!last) return FSE_OK;
+    out[n - 1u] = (uint8_t)dte_sym(dt[s]);  // Decoder::finish (lib.rs:208)
+    return br.pos == hdr_bits ? FSE_OK : FSE_ERR_BAD_SIDECAR;
+}
+
+// ------------------------------------------------------------------------
+// Segment decode of a block staged in LDS (L <= 12, SH = 18).  One LdsChain
+// is one segment's decoder pair: two tANS states as LDS byte offsets
+// a0/a1 (4 * state) and the shared bit position.  Per pair the lane reads
+// both table entries and ONE payload dword, all three issued together:
+// a pair consumes <= 24 < 32 bits, so the window base lo = (pos - 24) & ~31
+// moves down by at most one word per pair and the window's upper word is
+// one of the previous pair's two words.  Then pos -= nb0 + nb1 (byte sum of
+// the entries), v1 = the low nb1 bits at pos, v0 = the nb0 bits above
+// (stack order: decoder 0 pops first), and the next offsets.  ~13 VALU and
+// 3 LDS reads per pair, no branch.  The image has a 16-byte pad below it,
+// so the window may start at word -1.
+// ------------------------------------------------------------------------
+struct LdsChain {
+    int32_t pos, B;
+    uint32_t whi, wlo, a0, a1;
+    __device__ __forceinline__ void init(const uint32_t* pay, int32_t p, uint32_t s0, uint32_t s1) {
+        pos = p;
+        a0 = s0 << 2;
+        a1 = s1 << 2;
+        // the first pair reads word lo/32 and takes word lo/32 + 1 from here
+        B = (p - 24) & ~31;
+        wlo = 0;
+        whi = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(pay) + (B >> 3) + 4);
+    }
+    __device__ __forceinline__ uint32_t pair(const uint32_t* pay, const uint8_t* dtb) {
+        const int32_t lo = (pos - 24) & ~31;
+        const uint32_t w0 = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(pay) + (lo >> 3));
+        const uint32_t e0 = *reinterpret_cast<const uint32_t*>(dtb + a0);
+        const uint32_t e1 = *reinterpret_cast<const uint32_t*>(dtb + a1);
+        const uint32_t w1 = lo == B ? whi : wlo;
+        pos -= (int32_t)((e0 + e1) & 0xFFu);
+        const uint32_t x = (uint32_t)((((uint64_t)w1 << 32) | w0) >> (uint32_t)(pos - lo));
+        B = lo;
+        whi = w1;
+        wlo = w0;
+        const uint32_t v1 = __builtin_amdgcn_ubfe(x, 0u, e1);
+        const uint32_t v0 = __builtin_amdgcn_ubfe(x, e1, e0);
+        a0 = (e0 >> 16) + (v0 << 2);
+        a1 = (e1 >> 16) + (v1 << 2);
+        return __builtin_amdgcn_perm(e1, e0, 0x0c0c0501u);  // sym0 | sym1 << 8
+    }
+};
+
+// Bits [pos, pos + 32) of an LDS-staged block (pos >= 0): one ds_read2 of
+// the two words holding them and a v_alignbit (the end-of-block steps).
+__device__ __forceinline__ uint32_t lds_bits32(const uint32_t* pay, int32_t pos) {
+    const uint32_t* wp = pay + ((uint32_t)pos >> 5);
+    return __builtin_amdgcn_alignbit(wp[1], wp[0], (uint32_t)pos);
+}
+
+// 32 pairs = one whole 64-byte piece of output per lane, stored back to
+// back (full HBM write bursts instead of masked partial ones).
+__device__ __forceinline__ void store_group(uint8_t* __restrict__ dst, const uint32_t* w) {
+    uint4* o4 = reinterpret_cast<uint4*>(dst);
+#pragma unroll
+    for (uint32_t q = 0; q < DEC_GROUP / 8u; ++q) o4[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+}
+
+// Pairs [p, p1) of one chain, then (when `last`) the container-mode end.
+__device__ __forceinline__ int32_t run_chain(LdsChain& c, const uint32_t* pay, const uint8_t* dtb, uint32_t p,
+                                             uint32_t p1, bool last, uint32_t n, uint32_t Pm,
+                                             uint8_t* __restrict__ out, int32_t hdr_bits) {
+    for (; p + DEC_GROUP <= p1; p += DEC_GROUP) {
+        uint32_t w[DEC_GROUP / 2u];
+#pragma unroll
+        for (uint32_t j = 0; j < DEC_GROUP; j += 2u) {
+            const uint32_t lo = c.pair(pay, dtb);
+            const uint32_t hi = c.pair(pay, dtb);
+            w[j >> 1] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);  // lo.b0 lo.b1 hi.b0 hi.b1
+        }
+        store_group(out + 2u * p, w);
+    }
+    for (; p < p1; ++p) {
+        const uint32_t pr = c.pair(pay, dtb);
+        out[2u * p] = (uint8_t)pr;
+        out[2u * p + 1u] = (uint8_t)(pr >> 8);
+    }
+    if (!last) return FSE_OK;
+    // states as indices for the shared end; the chain keeps byte offsets
+    uint32_t s0 = c.a0 >> 2, s1 = c.a1 >> 2;
+    return finish2<11>(2u * Pm, n, s0, s1, c.pos, hdr_bits, out,
+                       [&](uint32_t s) { return *reinterpret_cast<const uint32_t*>(dtb + 4u * s); },
+                       [&](uint32_t nb) {
+                           c.pos -= (int32_t)nb;
+                           return __builtin_amdgcn_ubfe(lds_bits32(pay, c.pos), 0u, nb);
+                       });
+}
+
+// 1-state chain (fse_decompress blocks): one state, one symbol per step,
+// a per-lane 64-bit window over words (k, k+1) refilled a word at a time
+// with the next word prefetched a refill ahead.
+struct LdsChain1 {
+    int32_t pos, B;
+    uint32_t wlo, whi, wnx, a;
+    __device__ __forceinline__ void init(const uint32_t* pay, int32_t p, uint32_t s) {
+        pos = p;
+        a = s << 2;
+        const int32_t k = max((p >> 5) - 1, 0);
+        B = k << 5;
+        wlo = pay[k];
+        whi = pay[k + 1];
+        wnx = pay[max(k - 1, 0)];
+    }
+    // one symbol; returns the table entry (symbol in bits 8-15)
+    __device__ __forceinline__ uint32_t step(const uint32_t* pay, const uint8_t* dtb) {
+        const uint32_t e = *reinterpret_cast<const uint32_t*>(dtb + a);
+        pos -= (int32_t)(e & 0xFFu);
+        const uint32_t x = (uint32_t)((((uint64_t)whi << 32) | wlo) >> (uint32_t)(pos - B));
+        if (pos < B + 32) {
+            B -= 32;
+            whi = wlo;
+            wlo = wnx;
+            wnx = pay[max((B >> 5) - 1, 0)];
+        }
+        a = (e >> 16) + (__builtin_amdgcn_ubfe(x, 0u, e) << 2);
+        return e;
+    }
+};
+
+// Steps [p, p1) of one 1-state segment; the last segment then emits the
+// final state's symbol (container mode: the raw length ends the block, as
+// the reference's next read fails right there for a valid stream).
+__device__ __forceinline__ int32_t run_chain1(LdsChain1& c, const uint32_t* pay, const uint8_t* dtb, uint32_t p,
+                                              uint32_t p1, bool last, uint32_t n, uint8_t* __restrict__ out,
+                                              int32_t hdr_bits) {
+    constexpr uint32_t G = 2u * DEC_GROUP;  // 64 symbols = one 64-byte piece of output
+    for (; p + G <= p1; p += G) {
+        uint32_t w[G / 4u];
+#pragma unroll
+        for (uint32_t j = 0; j < G; j += 4u) {
+            const uint32_t e0 = c.step(pay, dtb), e1 = c.step(pay, dtb);
+            const uint32_t e2 = c.step(pay, dtb), e3 = c.step(pay, dtb);
+            w[j >> 2] = __builtin_amdgcn_perm(__builtin_amdgcn_perm(e3, e2, 0x0c0c0501u),
+                                              __builtin_amdgcn_perm(e1, e0, 0x0c0c0501u), 0x05040100u);
+        }
+        uint4* o4 = reinterpret_cast<uint4*>(out + p);
+#pragma unroll
+        for (uint32_t q = 0; q < G / 16u; ++q) o4[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+    }
+    for (; p < p1; ++p) out[p] = (uint8_t)dte_sym(c.step(pay, dtb));
+    if (!last) return FSE_OK;
+    out[n - 1u] = (uint8_t)dte_sym(*reinterpret_cast<const uint32_t*>(dtb + c.a));  // finish (lib.rs:208)
+    return c.pos == hdr_bits ? FSE_OK : FSE_ERR_BAD_SIDECAR;
+}
+
+// ------------------------------------------------------------------------
+// Segment-parallel decode with prebuilt tables (fsehip_decompress_blocks_dt,
+// the second kernel of fsehip_decompress_blocks; C3 times it alone).  One
+// 256-thread workgroup per block:
+//   1. DMA (global_load_lds) the compressed block and its table into LDS;
+//   2. lane t decodes sidecar segment 33t mod 256 of each round (lanes that
+//      walk their segments in lockstep then read payload words ~33 segments
+//      apart, spread over the banks, instead of ~1 segment apart), storing
+//      32 pairs (64 B) at a time;
+//   3. every segment's end is checked against the next checkpoint.
+// Blocks above the PMAX-byte stage are deferred (pass 1: status
+// FSE_DEFERRED) to a second launch with a 66 KiB stage (pass 2); at
+// LMAX > 12 the table alone fills the LDS and every block reads its payload
+// through a global-memory window (pass 0).
+// ------------------------------------------------------------------------
+template <int LMAX, uint32_t PMAX>
+struct PreSmem {
+    uint32_t pad[4];  // below the image: the window may start at word -1
+    uint32_t pay[PMAX / 4];
+    uint32_t dt[1u << LMAX];
+    int err[4];
+};
+
+template <int LMAX, uint32_t PMAX, int NS>
+__global__ __launch_bounds__(256) void decode_pre_kernel(DecParams P) {
+    constexpr bool BIG = LMAX > 12;  // no LDS image
+    constexpr uint32_t NT = 256u, NW = 4u;
+    __shared__ PreSmem<LMAX, BIG ? 16u : PMAX> sm;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    const uint64_t gb = blockIdx.x;
+    if (gb >= P.n_blocks) return;
+    const uint8_t* in = P.in + gb * P.slot_bytes;
+    const uint32_t clen = P.comp_len[gb];
+    const uint64_t ooff = gb * (uint64_t)P.block_size;
+    const uint32_t n = (uint32_t)min((uint64_t)P.block_size, P.n_total - ooff);
+    uint8_t* out = P.out + ooff;
+    const int32_t info = P.dtinfo[gb];
+    const bool in_lds = !BIG && clen <= PMAX;
+    if (P.pass == 2 && P.status[gb] != FSE_DEFERRED) return;  // done by the first pass
+    FSE_STAMP(P, 0);
+    if (info < 0 || n < (NS == 2 ? 2u : 1u)) {
+        if (tid == 0) P.status[gb] = info < 0 ? info : FSE_ERR_LENGTH_MISMATCH;
+        return;
+    }
+    if (P.pass == 1 && !in_lds) {  // too big for this stage: the big-stage pass decodes it
+        if (tid == 0) P.status[gb] = FSE_DEFERRED;
+        return;
+    }
+    const int32_t hdr_bits = (info & 0xFFFF) * 8;
+    const uint32_t L = (uint32_t)info >> 16;
+    {  // stage the block image and the table
+        if (in_lds) {
+            const uint32_t nvec = (clen + 15u) >> 4;
+            const uint4* src4 = reinterpret_cast<const uint4*>(in);
+            uint4* dst4 = reinterpret_cast<uint4*>(sm.pay);
+            for (uint32_t i = wv * 64u; i < nvec; i += NT)
+                if (i + lane < nvec) __builtin_amdgcn_global_load_lds(src4 + i + lane, dst4 + i, 16, 0, 0);
+        }
+        const uint32_t dvec = 1u << L >> 2;  // 4 << L bytes
+        const uint4* t4 = reinterpret_cast<const uint4*>(P.dt + gb * (uint64_t)(1u << LMAX));
+        uint4* d4 = reinterpret_cast<uint4*>(sm.dt);
+        for (uint32_t i = wv * 64u; i < dvec; i += NT)
+            if (i + lane < dvec) __builtin_amdgcn_global_load_lds(t4 + i + lane, d4 + i, 16, 0, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    FSE_STAMP(P, 3);
+    const uint32_t smask = (1u << L) - 1u;
+    // main-loop steps: pairs (NS = 2) or symbols below the last one (NS = 1)
+    const uint32_t Pm = NS == 2 ? ((n & 1u) ? (n - 3u) / 2u : n / 2u - 1u) : n - 1u;
+    const uint32_t I = P.ckpt_interval;
+    const uint32_t nseg = Pm / I + 1u;
+    const uint64_t* sc = P.sidecar + gb * P.ckpt_per_block;
+    const uint32_t maxbp = clen * 8u - (uint32_t)hdr_bits;
+    const uint8_t* dtb = reinterpret_cast<const uint8_t*>(sm.dt);
+    const uint32_t* gw = reinterpret_cast<const uint32_t*>(in);
+    int32_t err = FSE_OK;
+    for (uint32_t base = 0; base < nseg; base += NT) {
+        const uint32_t seg = base + (NS == 2 ? ((tid * 33u) & (NT - 1u)) : tid);
+        if (seg >= nseg) continue;
+        const uint64_t e = sc[seg];
+        const uint32_t p0 = seg * I, p1 = min(p0 + I, Pm);
+        const uint32_t bp = (uint32_t)e;
+        uint32_t s0 = (uint32_t)(e >> 32) & smask, s1 = NS == 2 ? (uint32_t)(e >> 48) & smask : 0u;
+        const bool lastseg = seg == nseg - 1u;
+        const uint64_t en = lastseg ? 0ull : sc[seg + 1u];
+        int32_t r;
+        if (bp > maxbp) {  // corrupt index: never read outside the block
+            r = FSE_ERR_BAD_SIDECAR;
+        } else if (NS == 1) {
+            if (!BIG && in_lds) {
+                LdsChain1 c;
+                c.init(sm.pay, hdr_bits + (int32_t)bp, s0);
+                r = run_chain1(c, sm.pay, dtb, p0, p1, lastseg, n, out, hdr_bits);
+                if (r == FSE_OK && !lastseg && !ckpt_match(en, hdr_bits, smask, c.pos, c.a, 0u)) r = FSE_ERR_BAD_SIDECAR;
+            } else {
+                WindowReader br;
+                br.init(gw, hdr_bits + (int32_t)bp);
+                r = decode_segment1<LMAX>(br, s0, p0, p1, lastseg, n, out, sm.dt, hdr_bits);
+                if (r == FSE_OK && !lastseg && !ckpt_match(en, hdr_bits, smask, br.pos, s0 << 2, 0u))
+                    r = FSE_ERR_BAD_SIDECAR;
+            }
+        } else if (!BIG && in_lds) {
+            LdsChain c;
+            c.init(sm.pay, hdr_bits + (int32_t)bp, s0, s1);
+            r = run_chain(c, sm.pay, dtb, p0, p1, lastseg, n, Pm, out, hdr_bits);
+            if (r == FSE_OK && !lastseg && !ckpt_match(en, hdr_bits, smask, c.pos, c.a0, c.a1)) r = FSE_ERR_BAD_SIDECAR;
+        } else {
+            WindowReader br;
+            br.init(gw, hdr_bits + (int32_t)bp);
+            r = decode_segment<LMAX>(br, s0, s1, p0, p1, lastseg, n, Pm, out, sm.dt, hdr_bits);
+            if (r == FSE_OK && !lastseg && !ckpt_match(en, hdr_bits, smask, br.pos, s0 << 2, s1 << 2))
+                r = FSE_ERR_BAD_SIDECAR;
+        }
+        if (r != FSE_OK) err = r;
+    }
+    err = -(int32_t)wave_max((uint32_t)(-err));
+    if (lane == 0) sm.err[wv] = err;
+    __syncthreads();
+    FSE_STAMP(P, 4);
+    if (tid == 0) {
+        int32_t e2 = FSE_OK;
+        for (uint32_t w = 0; w < NW; ++w)
+            if (sm.err[w] != FSE_OK) e2 = sm.err[w];
+        P.status[gb] = e2;
+        if (P.out_len) P.out_len[gb] = e2 ? 0u : n;
+    }
+}
+
+// ------------------------------------------------------------------------
+// Decode tables for a batch of blocks (C3's "pre-built dtables"; also the
+// first kernel of the two-kernel decode): NormHistogram::read on the scalar
+// unit + DecodeTable (fse.rs:280-338) by one wave per block, written to HBM
+// in the decoder's entry layout.  Small LDS footprint at L <= 12, so many
+// blocks are in flight per CU and the serial header parse is overlapped
+// across blocks.
+// ------------------------------------------------------------------------
+template <int LMAX>
+__global__ __launch_bounds__(64) void dtable_blocks_kernel(DtParams P) {
+    constexpr uint32_t SIZE = 1u << LMAX;
+    __shared__ int32_t norm[256];
+    __shared__ __attribute__((aligned(16))) uint8_t sym_at[SIZE];
+    // the two-pass rank table (2^L u16) reuses the occurrence owners, the
+    // counters and cumul: all three are dead once the spread walk is done
+    // (the decoder's visit reads norm only); 7 KB per workgroup at L = 11
+    __shared__ __attribute__((aligned(16))) uint16_t rk[SIZE];
+    static_assert(SIZE + 256 * 4 + 256 * 2 <= SIZE * 2, "rank table must cover occ, cnt and cumul");
+    uint8_t* occ = reinterpret_cast<uint8_t*>(rk);
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(rk) + SIZE);
+    uint16_t* cumul = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(rk) + SIZE + 1024);
+    const uint32_t lane = lane_id();
+    const uint64_t gb = blockIdx.x;
+    if (gb >= P.n_blocks) return;
+    const uint8_t* in = P.in + gb * P.slot_bytes;
+    const uint32_t clen = P.comp_len[gb];
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(in);
+    // The header words are loaded before the length arrives when the slot
+    // holds HDR_MAX bytes (always, for encoder slots), so the two loads and
+    // the marker byte's load overlap instead of following one another;
+    // words past the block are zeroed once the length is known.
+    uint32_t r0, r1;
+    if (P.slot_bytes >= HDR_MAX) {
+        r0 = w[lane];
+        r1 = w[lane + 64u];
+    }
+    const uint32_t last = (clen && clen <= P.slot_bytes) ? in[clen - 1u] : 0u;
+    const uint32_t nw = (uint32_t)min((uint64_t)min(clen, HDR_MAX) + 3u, P.slot_bytes) >> 2;
+    if (P.slot_bytes < HDR_MAX) {
+        r0 = lane < nw ? w[lane] : 0u;
+        r1 = lane + 64u < nw ? w[lane + 64u] : 0u;
+    }
+    r0 = lane < nw ? r0 : 0u;
+    r1 = lane + 64u < nw ? r1 : 0u;
+    for (uint32_t s = lane; s < 256u; s += WAVE) norm[s] = 0;
+    wave_sync();
+    uint32_t L = 0, tl = 0;
+    const int hl = header_read_wave(r0, r1, clen, (uint32_t)LMAX, norm, &L, &tl);
+    int rc = hl < 0 ? hl : FSE_OK;
+    if (rc == FSE_OK && ((uint32_t)hl >= clen || last == 0)) rc = FSE_ERR_NO_MARKER;  // lib.rs:222
+    wave_sync();
+    if (rc == FSE_OK) {
+        const uint32_t size = 1u << L;
+        uint32_t* dt = P.dt + gb * (uint64_t)SIZE;
+        auto visit = [&](uint32_t i, uint32_t s, uint32_t r) {
+            const int32_t v = norm[s];
+            const uint32_t nx = (v < 0 ? 1u : (uint32_t)v) + r;
+            const uint32_t nb = L - ilog2u(nx);
+            dt[i] = Dte<LMAX>::make(nb, s, (nx << nb) - size);
+        };
+        // two-pass ranks need 2^L / 64 per-chunk registers: up to L = 12
+        if (LMAX <= 12) rc = wave_build_spread<SIZE / 64u>(norm, L, tl, sym_at, occ, cumul, cnt, visit, rk);
+        else rc = wave_build_spread(norm, L, tl, sym_at, occ, cumul, cnt, visit);
+    }
+    if (lane == 0) P.dtinfo[gb] = rc == FSE_OK ? (int32_t)((uint32_t)hl | (L << 16)) : rc;
+}
+
+// ------------------------------------------------------------------------
+// fse_decompress (lib.rs:187-211) without a sidecar: one lane per block
+// walks the stream with every read checked, on tables from
+// dtable_blocks_kernel.  Container mode (raw length known) or the
+// reference's own termination with a capacity (host streams).
+// ------------------------------------------------------------------------
+template <int LMAX>
+__global__ __launch_bounds__(64) void decode1_serial_kernel(DecParams P) {
+    const uint64_t gb = blockIdx.x;
+    if (gb >= P.n_blocks || threadIdx.x != 0) return;
+    const int32_t info = P.dtinfo[gb];
+    if (info < 0) {
+        P.status[gb] = info;
+        if (P.out_len) P.out_len[gb] = 0;
+        return;
+    }
+    const uint8_t* in = P.in + gb * P.slot_bytes;
+    const uint32_t clen = P.comp_len[gb];
+    const int32_t hdr_bits = (info & 0xFFFF) * 8;
+    const uint32_t L = (uint32_t)info >> 16;
+    const uint32_t* dt = P.dt + gb * (uint64_t)(1u << LMAX);
+    uint8_t* out = P.out + gb * (uint64_t)P.block_size;
+    const bool known = P.n_total != 0;  // container length, else reference mode with a capacity
+    const uint32_t n = known ? (uint32_t)min((uint64_t)P.block_size, P.n_total - gb * (uint64_t)P.block_size) : 0u;
+    const uint32_t cap = known ? n : P.out_cap;
+    int32_t err = FSE_OK;
+    uint32_t o = 0;
+    const int32_t top = (int32_t)(clen - 1u) * 8 + (int32_t)ilog2u(in[clen - 1]);  // marker (BitStackReader::new)
+    WindowReader br;
+    br.init(reinterpret_cast<const uint32_t*>(in), top);
+    if (br.pos - (int32_t)L < hdr_bits) {
+        err = FSE_ERR_TOO_SHORT;  // lib.rs:197 unwrap
+    } else {
+        uint32_t s = br.pop(L);
+        br.refill();
+        for (;;) {
+            const uint32_t e = dt[s];
+            const uint32_t nb = dte_nb(e);
+            if (br.pos - (int32_t)nb < hdr_bits) break;  // decode_symbol -> None
+            if (o >= cap) {  // nb == 0 forever: a probability-1 symbol never ends in the reference
+                err = nb == 0 ? FSE_ERR_SINGLE_SYMBOL : FSE_ERR_DST_TOO_SMALL;
+                break;
+            }
+            s = Dte<LMAX>::ns(e) + br.pop(nb);
+            br.refill();
+            out[o++] = (uint8_t)dte_sym(e);
+        }
+        if (err == FSE_OK) {
+            if (o >= cap) err = FSE_ERR_DST_TOO_SMALL;
+            else out[o++] = (uint8_t)dte_sym(dt[s]);  // Decoder::finish (lib.rs:208)
+        }
+        if (known && (err == FSE_ERR_DST_TOO_SMALL || (err == FSE_OK && o != n))) err = FSE_ERR_LENGTH_MISMATCH;
+    }
+    P.status[gb] = err;
+    if (P.out_len) P.out_len[gb] = err ? 0u : o;
+}
+
+// ------------------------------------------------------------------------
+// Sidecar-less decode of 2-state blocks (any valid fse_compress2 stream,
+// e.g. from the CPU crate), optionally recording the sidecar.  The two
+// interleaved decoders make the stream essentially serial: a decoder
+// started mid-block with guessed states practically never falls into step
+// with the exact one (oracle/syncsim.py: 35 of 40 random starts in a C2
+// block never did, the rest after 25K-40K symbols), so speculative segment
+// decoding cannot replace the sidecar for this format.  The
+// serial decode is instead made as short a dependency chain as possible and
+// run at high occupancy: the block's prebuilt table sits in LDS (8 KiB ->
+// 20 blocks in flight per CU), one lane walks the stream (lib.rs:227-244)
+// and the bits come through a register window fed from 16-byte chunks
+// loaded a whole chunk ahead.
+//   Container mode (n_total > 0): the raw length ends the block, as the
+//   oracle's decompress2 with a known length.
+//   Reference mode (n_total == 0, the host fse_decompress2): the block ends
+//   where a decoder's read fails (lib.rs:228-243), within out_cap bytes; a
+//   single-symbol table never ends in the reference and is refused.
+// ------------------------------------------------------------------------
+struct ChunkReader {
+    const uint4* w4;  // the block as 16-byte quads
+    uint64_t buf;     // stream bits [base, base + 64)
+    int32_t base, pos;
+    uint4 cl, ch, nl, nh;  // chunk c (words 8c..8c+7) and chunk c-1, loading
+    int32_t c;
+    __device__ __forceinline__ void init(const uint8_t* in, int32_t p) {
+        w4 = reinterpret_cast<const uint4*>(in);
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(in);
+        pos = p;
+        base = max(((p + 31) & ~31) - 64, 0);
+        buf = (uint64_t)w[base >> 5] | ((uint64_t)w[(base >> 5) + 1] << 32);
+        c = ((base >> 5) - 1) >> 3;  // chunk of the next word to enter the window
+        cl = w4[2 * max(c, 0)];
+        ch = w4[2 * max(c, 0) + 1];
+        nl = w4[2 * max(c - 1, 0)];
+        nh = w4[2 * max(c - 1, 0) + 1];
+    }
+    __device__ __forceinline__ uint32_t pop(uint32_t nb) {
+        pos -= (int32_t)nb;
+        return (uint32_t)(buf >> (uint32_t)(pos - base)) & ((1u << nb) - 1u);
+    }
+    __device__ __forceinline__ void refill() {
+        if (pos - base < 32 && base > 0) {
+            base -= 32;
+            const int32_t wi = base >> 5;
+            if ((wi >> 3) != c) {  // every 8th refill: move down a chunk, prefetch the next
+                cl = nl;
+                ch = nh;
+                c -= 1;
+                nl = w4[2 * max(c - 1, 0)];
+                nh = w4[2 * max(c - 1, 0) + 1];
+            }
+            const uint32_t j = (uint32_t)wi & 7u;
+            const uint4 q = j < 4u ? cl : ch;
+            const uint32_t k = j & 3u;
+            const uint32_t v = k == 0 ? q.x : k == 1 ? q.y : k == 2 ? q.z : q.w;
+            buf = (buf << 32) | v;
+        }
+    }
+};
+
+template <int LMAX>
+__global__ __launch_bounds__(64) void serial2_decode_kernel(DecParams P) {
+    __shared__ uint32_t tab[1u << LMAX];
+    const uint64_t gb = blockIdx.x;
+    if (gb >= P.n_blocks) return;
+    const int32_t info = P.dtinfo[gb];
+    const uint32_t lane = threadIdx.x;
+    uint32_t nbor = 0;  // OR of the staged entries' nb: 0 = single-symbol table
+    if (info >= 0) {  // stage the table (prebuilt by dtable_blocks_kernel)
+        const uint32_t nv = (1u << ((uint32_t)info >> 16)) >> 2;  // 16-byte chunks
+        const uint4* t4 = reinterpret_cast<const uint4*>(P.dt + gb * (uint64_t)(1u << LMAX));
+        uint4* d4 = reinterpret_cast<uint4*>(tab);
+        for (uint32_t i = lane; i < nv; i += 64u) {
+            const uint4 q = t4[i];
+            d4[i] = q;
+            nbor |= (q.x | q.y | q.z | q.w) & 0xFFu;
+        }
+    }
+    const bool single = __ballot(nbor != 0u) == 0ull;
+    __syncthreads();
+    if (lane != 0) return;
+    const uint8_t* in = P.in + gb * P.slot_bytes;
+    const uint32_t clen = P.comp_len[gb];
+    const bool known = P.n_total != 0;
+    const uint64_t ooff = gb * (uint64_t)P.block_size;
+    const uint32_t n = known ? (uint32_t)min((uint64_t)P.block_size, P.n_total - ooff) : 0u;
+    const uint32_t lim = known ? n : P.out_cap;  // bytes the block may produce
+    uint8_t* out = P.out + ooff;
+    int32_t err = info < 0 ? info : FSE_OK;
+    if (err == FSE_OK && known && n < 2) err = FSE_ERR_LENGTH_MISMATCH;
+    if (err == FSE_OK && !known && single) err = FSE_ERR_SINGLE_SYMBOL;  // the reference loops forever
+    const int32_t hdr_bits = (info & 0xFFFF) * 8;
+    const uint32_t L = (uint32_t)info >> 16;
+    uint32_t o = 0;
+    if (err == FSE_OK) {
+        const int32_t top = (int32_t)(clen - 1u) * 8 + (int32_t)ilog2u(in[clen - 1]);
+        if (top - 2 * (int32_t)L < hdr_bits) err = FSE_ERR_TOO_SHORT;  // lib.rs:224-225
+    }
+    if (err == FSE_OK) {
+        ChunkReader br;
+        br.init(in, (int32_t)(clen - 1u) * 8 + (int32_t)ilog2u(in[clen - 1]));
+        uint32_t s0 = br.pop(L);
+        br.refill();
+        uint32_t s1 = br.pop(L);
+        br.refill();
+        const uint32_t I = P.ckpt_interval;
+        uint64_t* rec = (P.sidecar_out && I) ? P.sidecar_out + gb * P.ckpt_per_block : nullptr;
+        const uint32_t ckmask = I ? I - 1u : 0u;
+        uint32_t pidx = 0;
+        auto record = [&]() {
+            if (rec && (pidx & ckmask) == 0u && pidx / I < P.ckpt_per_block)
+                rec[pidx / I] = (uint64_t)(uint32_t)(br.pos - hdr_bits) | ((uint64_t)s0 << 32) | ((uint64_t)s1 << 48);
+        };
+        // bulk: groups of 8 pairs that can neither reach the raw length (or
+        // the capacity) nor run out of bits (<= 2L bits a pair): no end
+        // checks, and the 16 output bytes leave as one dwordx4 store, so few
+        // stores are in flight when the next chunk's load is waited on
+        while (o + 18u < lim && br.pos - hdr_bits >= 16 * (int32_t)L) {
+            uint32_t w[4];
+#pragma unroll
+            for (uint32_t j = 0; j < 8u; ++j, ++pidx) {
+                record();
+                const uint32_t e0 = tab[s0];
+                s0 = Dte<LMAX>::ns(e0) + br.pop(dte_nb(e0));
+                br.refill();
+                const uint32_t e1 = tab[s1];
+                s1 = Dte<LMAX>::ns(e1) + br.pop(dte_nb(e1));
+                br.refill();
+                const uint32_t v = dte_sym(e0) | (dte_sym(e1) << 8);
+                if (j & 1u) w[j >> 1] |= v << 16; else w[j >> 1] = v;
+            }
+            *reinterpret_cast<uint4*>(out + o) = make_uint4(w[0], w[1], w[2], w[3]);
+            o += 16;
+        }
+        // tail: pair by pair with the reference's end checks
+        const int32_t full = known ? FSE_ERR_LENGTH_MISMATCH : FSE_ERR_DST_TOO_SMALL;
+        for (;; ++pidx) {
+            record();
+            if (known && o + 2u >= n) {  // the raw length ends the block (o is even here)
+                if (o < n) out[o++] = (uint8_t)dte_sym(tab[s0]);
+                if (o < n) out[o++] = (uint8_t)dte_sym(tab[s1]);
+                break;
+            }
+            const uint32_t e0 = tab[s0];
+            uint32_t nb = dte_nb(e0);
+            if (br.pos - (int32_t)nb < hdr_bits) {  // decoder 0 cannot read: lib.rs:242-243
+                if (o + 2u > lim) { err = full; break; }
+                out[o++] = (uint8_t)dte_sym(e0);
+                out[o++] = (uint8_t)dte_sym(tab[s1]);
+                break;
+            }
+            s0 = Dte<LMAX>::ns(e0) + br.pop(nb);
+            br.refill();
+            if (o >= lim) { err = full; break; }
+            out[o++] = (uint8_t)dte_sym(e0);
+            const uint32_t e1 = tab[s1];
+            nb = dte_nb(e1);
+            if (br.pos - (int32_t)nb < hdr_bits) {  // decoder 1 cannot read: lib.rs:235-239
+                if (o + 2u > lim) { err = full; break; }
+                out[o++] = (uint8_t)dte_sym(e1);
+                out[o++] = (uint8_t)dte_sym(tab[s0]);
+                break;
+            }
+            s1 = Dte<LMAX>::ns(e1) + br.pop(nb);
+            br.refill();
+            if (o >= lim) { err = full; break; }
+            out[o++] = (uint8_t)dte_sym(e1);
+        }
+        if (err == FSE_OK && known && o != n) err = FSE_ERR_LENGTH_MISMATCH;
+    }
+    P.status[gb] = err;
+    if (P.out_len) P.out_len[gb] = err ? 0u : o;
+}
+
+// ------------------------------------------------------------------------
+// launch wrappers
+// ------------------------------------------------------------------------
+hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) {
+    const dim3 g(P.n_blocks);
+    if (!P.dt || !P.dtinfo) return hipErrorInvalidValue;
+    if (!P.sidecar) {  // serial: sidecar-less blocks, reference-mode host streams, sidecar recording
+        if (P.nstates == 1) {
+            if (lmax <= 11) hipLaunchKernelGGL((decode1_serial_kernel<11>), g, dim3(64), 0, stream, P);
+            else if (lmax <= 12) hipLaunchKernelGGL((decode1_serial_kernel<12>), g, dim3(64), 0, stream, P);
+            else hipLaunchKernelGGL((decode1_serial_kernel<15>), g, dim3(64), 0, stream, P);
+        } else {
+            if (lmax <= 11) hipLaunchKernelGGL((serial2_decode_kernel<11>), g, dim3(64), 0, stream, P);
+            else if (lmax <= 12) hipLaunchKernelGGL((serial2_decode_kernel<12>), g, dim3(64), 0, stream, P);
+            else hipLaunchKernelGGL((serial2_decode_kernel<15>), g, dim3(64), 0, stream, P);
+        }
+        return hipGetLastError();
+    }
+    // segment-parallel: LDS = image + table (44 KiB image at L <= 11 -> 3
+    // workgroups per CU); blocks above the stage (e.g. near-uniform data,
+    // ~65 KB) are deferred to a second launch with a 66 KiB stage (2
+    // workgroups per CU) instead of the global-memory reader
+    constexpr uint32_t PP = 44u << 10, PB = 66u << 10;
+    DecParams P1 = P, P2 = P;
+    P1.pass = 1;
+    P2.pass = 2;
+    auto two = [&](auto k1, auto k2) {
+        hipLaunchKernelGGL(k1, g, dim3(256), 0, stream, P1);
+        hipLaunchKernelGGL(k2, g, dim3(256), 0, stream, P2);
+    };
+    DecParams P0 = P;
+    P0.pass = 0;
+    if (P.nstates == 1) {
+        if (lmax <= 11) two(decode_pre_kernel<11, PP, 1>, decode_pre_kernel<11, PB, 1>);
+        else if (lmax <= 12) two(decode_pre_kernel<12, PP - 8192, 1>, decode_pre_kernel<12, PB, 1>);
+        else hipLaunchKernelGGL((decode_pre_kernel<15, 16, 1>), g, dim3(256), 0, stream, P0);
+    } else {
+        if (lmax <= 11) two(decode_pre_kernel<11, PP, 2>, decode_pre_kernel<11, PB, 2>);
+        else if (lmax <= 12) two(decode_pre_kernel<12, PP - 8192, 2>, decode_pre_kernel<12, PB, 2>);
+        else hipLaunchKernelGGL((decode_pre_kernel<15, 16, 2>), g, dim3(256), 0, stream, P0);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_dtables(const DtParams& P, uint32_t lmax, hipStream_t stream) {
+    const dim3 g(P.n_blocks), b(64);
+    if (lmax <= 11) hipLaunchKernelGGL((dtable_blocks_kernel<11>), g, b, 0, stream, P);
+    else if (lmax <= 12) hipLaunchKernelGGL((dtable_blocks_kernel<12>), g, b, 0, stream, P);
+    else hipLaunchKernelGGL((dtable_blocks_kernel<15>), g, b, 0, stream, P);
+    return hipGetLastError();
+}
+
+}  // namespace fsehip

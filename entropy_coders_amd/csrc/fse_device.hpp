@@ -13,6 +13,13 @@
 
 namespace fsehip {
 
+// Diagnostic phase stamps (only when P.stamps is set by the host).
+#define FSE_STAMP(P, slot)                                                                     \
+    do {                                                                                       \
+        if ((P).stamps && threadIdx.x == 0)                                                    \
+            (P).stamps[(uint64_t)blockIdx.x * kStamps + (slot)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+
 constexpr uint32_t LOG_MIN = 5;       // lib.rs:9
 constexpr uint32_t LOG_MAX_REF = 15;  // lib.rs:10
 constexpr uint32_t LOG_DEFAULT = 11;  // lib.rs:12
@@ -382,7 +389,8 @@ struct ByteWriter {
     }
 };
 
-__device__ inline int header_write_lane(const int32_t* norm, uint32_t L, uint32_t tl, uint8_t* hdr) {
+__device__ inline int header_write_lane(const int32_t* norm, uint32_t L, uint32_t tl, uint8_t* hdr,
+                                       uint32_t* bits_out = nullptr) {
     ByteWriter w{hdr, 0, 0, 0, false};
     w.put(L - LOG_MIN, 4);
     int32_t thr = 1 << L;
@@ -408,6 +416,7 @@ __device__ inline int header_write_lane(const int32_t* norm, uint32_t L, uint32_
         if (rem < 1) return FSE_ERR_BAD_TABLE;
         while (rem < thr) { nb -= 1; thr >>= 1; }
     }
+    if (bits_out) *bits_out = w.byte * 8u + w.nacc;  // BitStackWriter::finish's count (writer.rs:201-222)
     uint32_t len = w.finish();
     if (w.overflow) return FSE_ERR_DST_TOO_SMALL;
     return (int)len;

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/fsehip.h"
+
 namespace fsehip {
 
 struct EncParams {
@@ -25,15 +27,6 @@ struct EncParams {
     uint32_t debug;  // ablation: bit0 = tables only, bit1 = no emit pass, bit2 = no payload stores,
                      // bit3 = histogram only, bit4 = no repair rounds
     uint64_t* stamps;  // diagnostics: per-workgroup s_memtime at phase ends
-    // Scratch-emit path (see encode_blocks_kernel): each lane writes its
-    // bits to a lane-private scratch stream from the start state the count
-    // pass gives it, and a copy pass moves the streams to their final bit
-    // offsets once the exact lengths are known.  nullptr = repair path only.
-    uint32_t* scratch;        // [n_blocks][lanes][scr_lane_words]
-    uint32_t scr_lane_words;  // words per lane stream (worst case, multiple of 32)
-    uint32_t warm;            // count-pass warm-up pairs above the lane's range (scratch path)
-    uint32_t path;            // 0 = by distribution, 1 = repair path, 2 = scratch path
-    uint32_t pmax256;         // auto: scratch path when max norm <= pmax256/256 of the table
     uint32_t xlds;            // diagnostics: extra dynamic LDS bytes per workgroup (occupancy probe)
 };
 
@@ -52,15 +45,10 @@ struct DecParams {
     int32_t* status;
     uint32_t* out_len;
     uint64_t* sidecar_out;  // serial mode: record checkpoints here
-    uint32_t debug;         // ablation: bit0 = header + table only
     uint64_t* stamps;       // diagnostics: per-workgroup s_memtime at phase ends
-    uint32_t waves;         // waves per block workgroup: 4 (default) or 8
-    const uint32_t* dt;     // prebuilt decode tables [n_blocks][1 << lmax], or nullptr
+    const uint32_t* dt;     // prebuilt decode tables [n_blocks][1 << lmax] (dtable_blocks_kernel)
     const int32_t* dtinfo;  // per block: header bytes | L << 16, or < 0 = status
-    uint32_t variant;       // LDS layout / reader: 3/5 = padded image (prebuilt tables), else linear window
-    uint32_t dual;          // two segments per lane, interleaved (prebuilt-table kernel)
-    uint32_t stage_kib;     // LDS image size of the prebuilt-table kernel: 44 (default), 40 or 36 KiB
-    uint32_t pass;          // prebuilt-table kernel: 0 = all blocks, 1 = defer blocks the stage cannot
+    uint32_t pass;          // segment decode: 0 = all blocks, 1 = defer blocks the LDS stage cannot
                             // hold (status FSE_DEFERRED), 2 = only the deferred blocks (big stage)
     uint32_t nstates;       // 2 = fse_compress2 blocks (default), 1 = fse_compress blocks
 };
@@ -73,7 +61,6 @@ struct DtParams {
     uint32_t n_blocks;
     uint32_t* dt;      // [n_blocks][1 << lmax] entries (dte_make layout)
     int32_t* dtinfo;   // header bytes | L << 16, or < 0 = status
-    uint32_t debug;    // ablation: bit0 = header parse only, bit1 = no table stores
 };
 
 struct GenParams {
@@ -86,11 +73,41 @@ struct GenParams {
     uint16_t bound[1024];
 };
 
+// Building blocks (fse_blocks.hip): normalisation of one histogram.
+struct NormArgs {
+    int mode;                // 0 = Histogram::normalize(log2), 1 = normalize_optimal, 2 = NormHistogram::new(src)
+    const uint8_t* src;      // mode 2: raw bytes
+    uint64_t n;
+    const uint32_t* counts;  // modes 0/1: counts[256]
+    uint32_t size, table_len, log2;
+    fse_norm_histogram* out;
+    uint32_t* counts_out;    // optional: counts[256], size, table_len (mode 2's histogram)
+    int32_t* status;
+};
+hipError_t launch_norm(const NormArgs& A, hipStream_t s);
+hipError_t launch_hdr_write(const fse_norm_histogram* nh, uint8_t* out, uint32_t* bits, int32_t* status, hipStream_t s);
+hipError_t launch_hdr_read(const uint8_t* src, uint32_t n, fse_norm_histogram* out, uint32_t* used, int32_t* status,
+                           hipStream_t s);
+hipError_t launch_table(const fse_norm_histogram* nh, int enc, fse_encode_table* et, fse_decode_table* dt,
+                        int32_t* status, hipStream_t s);
+// Bitstream primitives: a tile scan of the field widths (tile_sum: u32 per
+// tile, tile_off: u64 per tile, total: u64), then pack or unpack.
+uint64_t bits_tiles(uint64_t count);
+hipError_t launch_bits_scan(const uint8_t* nbits, uint64_t count, uint32_t* tile_sum, uint64_t* tile_off,
+                            uint64_t* total, hipStream_t s);
+hipError_t launch_bits_pack(const uint32_t* vals, const uint8_t* nbits, uint64_t count, const uint64_t* tile_off,
+                            const uint64_t* total, uint32_t* out, uint64_t lim_words, hipStream_t s);
+hipError_t launch_bits_unpack(const uint8_t* in, uint64_t n_bytes, uint64_t total_bits, int stack,
+                              const uint8_t* nbits, uint64_t count, const uint64_t* tile_off, const uint64_t* total,
+                              uint32_t* vals, uint64_t* result, hipStream_t s);
+
 constexpr int kStamps = 10;  // stamp slots per workgroup
 constexpr int32_t FSE_DEFERRED = 1;  // internal block status between the two decode passes
 
 hipError_t launch_encode(const EncParams& P, uint32_t lmax, hipStream_t stream);
 hipError_t launch_dtables(const DtParams& P, uint32_t lmax, hipStream_t stream);
+// lmax: 11 (blocks of L <= 11), 12 or 15 (L 13..15); decode tables are laid
+// out at that stride (4 << lmax bytes per block).
 hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream);
 // Diagnostics: resident workgroups per CU of the main kernels, as text.
 int occupancy_report(char* buf, int cap);

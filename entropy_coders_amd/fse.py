@@ -10,7 +10,7 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import FseError, Params, check, load
+from ._lib import (DecodeTable, EncodeTable, FseError, Histogram, NormHistogram, Params, check, load)
 
 
 def _buf(data) -> np.ndarray:
@@ -90,6 +90,125 @@ def histogram_count(src) -> tuple[np.ndarray, int]:
     tl = C.c_uint32(0)
     check(lib.histogram_count(_p(a), len(a), _p(counts), C.byref(tl)), "histogram_count")
     return counts, tl.value
+
+
+# ---------------------------------------------------------------- building blocks
+def histogram_new(src) -> Histogram:
+    """`Histogram::new(data)` (histogram.rs:18-66)."""
+    a = _buf(src)
+    h = Histogram()
+    check(load().histogram_new(_p(a), len(a), C.byref(h)), "histogram_new")
+    return h
+
+
+def normalize(h: Histogram, log2: int) -> NormHistogram:
+    """`Histogram::normalize(log2)` (histogram.rs:95-155)."""
+    nh = NormHistogram()
+    check(load().histogram_normalize(C.byref(h), log2, C.byref(nh)), "histogram_normalize")
+    return nh
+
+
+def normalize_optimal(h: Histogram) -> NormHistogram:
+    """`Histogram::normalize_optimal` (histogram.rs:281-284)."""
+    nh = NormHistogram()
+    check(load().histogram_normalize_optimal(C.byref(h), C.byref(nh)), "histogram_normalize_optimal")
+    return nh
+
+
+def norm_histogram_new(src) -> NormHistogram:
+    """`NormHistogram::new(data)` (histogram.rs:299-303)."""
+    a = _buf(src)
+    nh = NormHistogram()
+    check(load().norm_histogram_new(_p(a), len(a), C.byref(nh)), "norm_histogram_new")
+    return nh
+
+
+def norm_histogram_write(nh: NormHistogram) -> tuple[bytes, int]:
+    """`NormHistogram::write(&mut Vec)` (histogram.rs:376-431): (bytes, bits written)."""
+    dst = np.zeros(1024, dtype=np.uint8)
+    n = C.c_size_t(0)
+    bits = C.c_uint64(0)
+    check(load().norm_histogram_write(C.byref(nh), _p(dst), len(dst), C.byref(n), C.byref(bits)),
+          "norm_histogram_write")
+    return dst[: n.value].tobytes(), bits.value
+
+
+def norm_histogram_read(data) -> tuple[NormHistogram, int]:
+    """`NormHistogram::read(slice)` (histogram.rs:436-505): (histogram, bytes consumed)."""
+    a = _buf(data)
+    nh = NormHistogram()
+    used = C.c_size_t(0)
+    check(load().norm_histogram_read(_p(a), len(a), C.byref(nh), C.byref(used)), "norm_histogram_read")
+    return nh, used.value
+
+
+def encode_table_new(nh: NormHistogram) -> EncodeTable:
+    """`EncodeTable::new(&hist)` (fse.rs:88-189) as plain data."""
+    t = EncodeTable()
+    check(load().encode_table_new(C.byref(nh), C.byref(t)), "encode_table_new")
+    return t
+
+
+def decode_table_new(nh: NormHistogram) -> DecodeTable:
+    """`DecodeTable::new(&hist)` (fse.rs:269-338) as plain data."""
+    t = DecodeTable()
+    check(load().decode_table_new(C.byref(nh), C.byref(t)), "decode_table_new")
+    return t
+
+
+def compress_nh(src) -> tuple[bytes, int, NormHistogram]:
+    """`fse_compress(src, &mut dst) -> (NormHistogram, usize)` (lib.rs:112) with
+    the histogram returned: (bytes, payload bits, NormHistogram)."""
+    a = _buf(src)
+    lib = load()
+    cap = int(lib.fsehip_slot_bytes(max(len(a), 16), 12))
+    dst = np.zeros(cap, dtype=np.uint8)
+    n = C.c_size_t(0)
+    bits = C.c_uint64(0)
+    nh = NormHistogram()
+    check(lib.fse_compress_nh(_p(a), len(a), _p(dst), cap, C.byref(n), C.byref(bits), C.byref(nh)), "fse_compress_nh")
+    return dst[: n.value].tobytes(), bits.value, nh
+
+
+# ---------------------------------------------------------------- bitstream
+def bitstack_write(vals, widths, prefix: bytes = b"") -> tuple[bytes, int]:
+    """BitStackWriter::new(&mut vec) over a vec holding `prefix`, then
+    write_bits_unmasked per field + finish (writer.rs:14-222): (the vec's
+    bytes, bits written)."""
+    v = np.ascontiguousarray(vals, dtype=np.uint32)
+    w = np.ascontiguousarray(widths, dtype=np.uint8)
+    cap = len(prefix) + len(v) * 4 + 16
+    dst = np.zeros(cap, dtype=np.uint8)
+    dst[: len(prefix)] = np.frombuffer(bytes(prefix), dtype=np.uint8)
+    n = C.c_size_t(len(prefix))
+    bits = C.c_uint64(0)
+    check(load().bitstack_write(_p(v), _p(w), len(v), _p(dst), cap, C.byref(n), C.byref(bits)), "bitstack_write")
+    return dst[: n.value].tobytes(), bits.value
+
+
+def bitstack_read(data, widths) -> tuple[list, int, bool]:
+    """BitStackReader::new + read(width) per field, top down (stack_reader.rs):
+    (values read, number of successful reads, finish())."""
+    a = _buf(data)
+    w = np.ascontiguousarray(widths, dtype=np.uint8)
+    out = np.zeros(max(len(w), 1), dtype=np.uint32)
+    nr = C.c_size_t(0)
+    fin = C.c_int(0)
+    check(load().bitstack_read(_p(a), len(a), _p(w), len(w), _p(out), C.byref(nr), C.byref(fin)), "bitstack_read")
+    return [int(x) for x in out[: nr.value]], nr.value, bool(fin.value)
+
+
+def bitstream_read(data, total_bits: int, widths) -> tuple[list, int, int]:
+    """BitStreamReader::new(slice, total_bits) + read(width) per field
+    (stream_reader.rs): (values read, number of successful reads, bits left)."""
+    a = _buf(data)
+    w = np.ascontiguousarray(widths, dtype=np.uint8)
+    out = np.zeros(max(len(w), 1), dtype=np.uint32)
+    nr = C.c_size_t(0)
+    left = C.c_uint64(0)
+    check(load().bitstream_read(_p(a), len(a), total_bits, _p(w), len(w), _p(out), C.byref(nr), C.byref(left)),
+          "bitstream_read")
+    return [int(x) for x in out[: nr.value]], nr.value, left.value
 
 
 class BlockCodec:
@@ -226,5 +345,7 @@ class BlockCodec:
         return cb["out"][s: s + ln].cpu().numpy().tobytes()
 
 
-__all__ = ["BlockCodec", "FseError", "compress", "compress2", "compress2_log", "decompress", "decompress2",
-           "histogram_count"]
+__all__ = ["BlockCodec", "DecodeTable", "EncodeTable", "FseError", "Histogram", "NormHistogram", "bitstack_read",
+           "bitstack_write", "bitstream_read", "compress", "compress2", "compress2_log", "compress_nh", "decode_table_new",
+           "decompress", "decompress2", "encode_table_new", "histogram_count", "histogram_new", "norm_histogram_new",
+           "norm_histogram_read", "norm_histogram_write", "normalize", "normalize_optimal"]

@@ -48,5 +48,15 @@
 #define FSE_ERR_UNSUPPORTED (-14)
 /* No HIP device / HIP extension not usable: product paths fail loudly.     */
 #define FSE_ERR_NO_DEVICE (-15)
+/* A decode checkpoint (sidecar entry) disagrees with the stream: a segment
+ * did not end at the next checkpoint's bit position and states, or the last
+ * segment did not consume the payload exactly (corrupt index, or one built
+ * with a different ckpt_interval).                                          */
+#define FSE_ERR_BAD_SIDECAR (-16)
+/* Encoder::new_first_symbol indexes outside the state table (fse.rs:212-216):
+ * at tableLog 15 its rounding constant 1 << 15 no longer covers the smallest
+ * state of a symbol with norm >= 2, the u32 subtraction wraps and the
+ * bounds-checked table read panics.                                         */
+#define FSE_ERR_ENCODER_INIT (-17)
 
 #endif

@@ -40,12 +40,14 @@ typedef void* fsehip_stream_t; /* hipStream_t; NULL = the null stream */
  * (lib.rs:146).  Appends header||payload at dst[*dst_len], advances
  * *dst_len, and stores the Rust return value (payload bits incl. marker) in
  * *payload_bits.  Errors: EMPTY, TOO_SHORT, ALL_ZERO_SYMBOL0 (reference
- * panics), DST_TOO_SMALL (the reference grows its Vec), UNSUPPORTED. */
+ * panics), DST_TOO_SMALL (the reference grows its Vec), UNSUPPORTED (n >
+ * 2^28), ENCODER_INIT (the tableLog-15 panic of new_first_symbol). */
 int fse_compress2(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, size_t* dst_len,
                   uint64_t* payload_bits);
 
 /* `Histogram::new(src).normalize(table_log)` followed by the fse_compress2
- * body (histogram.rs:95 + lib.rs:149-182): the tableLog sweep entry point. */
+ * body (histogram.rs:95 + lib.rs:149-182): the tableLog sweep entry point.
+ * table_log is clamped to 5..15 as normalize does (0 acts as 5). */
 int fse_compress2_log(const uint8_t* src, size_t n, uint32_t table_log, uint8_t* dst, size_t dst_cap,
                       size_t* dst_len, uint64_t* payload_bits);
 
@@ -68,15 +70,108 @@ int fse_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, s
 int histogram_count(const uint8_t* src, size_t n, uint32_t counts[256], uint32_t* table_len);
 
 /* ------------------------------------------------------------------------
+ * (1b) The crate's building blocks, as plain-data structs (repr(C) twins of
+ * the Rust types; every table has room for the largest log, 15) and calls
+ * that run on the GPU.  Same argument meaning and panics-as-statuses as
+ * above; host pointers.
+ * ------------------------------------------------------------------------ */
+
+/* Histogram (histogram.rs:9-14): counts, size = input length, table_len =
+ * 1 + the largest symbol (1 when empty). */
+typedef struct {
+    uint32_t counts[256];
+    uint32_t size;
+    uint32_t table_len;
+} fse_histogram;
+
+/* NormHistogram (histogram.rs:289-294): norm[s] in {-1, 0, 1..2^log2}. */
+typedef struct {
+    int32_t norm[256];
+    uint32_t log2;
+    uint32_t table_len;
+} fse_norm_histogram;
+
+/* EncodeTable (fse.rs:72-84): stateTable (`table`, 2^table_log used),
+ * the spread (`symbols`) and the symbol transforms. */
+typedef struct {
+    uint32_t bits;      /* deltaNbBits */
+    int32_t find_state; /* deltaFindState */
+} fse_symbol_transform;
+typedef struct {
+    uint32_t table_log;
+    uint16_t table[1u << 15];
+    uint8_t symbols[1u << 15];
+    fse_symbol_transform symbol_tt[256];
+} fse_encode_table;
+
+/* DecodeTable (fse.rs:253-265). */
+typedef struct {
+    uint16_t new_state;
+    uint8_t symbol;
+    uint8_t num_bits;
+} fse_decode_transform;
+typedef struct {
+    uint32_t table_log;
+    uint32_t fast_mode; /* no symbol with norm >= 2^(table_log-1) (fse.rs:302-305) */
+    fse_decode_transform table[1u << 15];
+} fse_decode_table;
+
+/* Histogram::new (histogram.rs:18-66). */
+int histogram_new(const uint8_t* src, size_t n, fse_histogram* out);
+/* Histogram::normalize(log2) (histogram.rs:95-155): log2 is clamped to 5..15
+ * and raised to ilog2(table_len - 1) + 2 as in the reference. */
+int histogram_normalize(const fse_histogram* h, uint32_t log2, fse_norm_histogram* out);
+/* Histogram::normalize_optimal (histogram.rs:281-284, optimal_log2 264-277). */
+int histogram_normalize_optimal(const fse_histogram* h, fse_norm_histogram* out);
+/* NormHistogram::new (histogram.rs:299-303). */
+int norm_histogram_new(const uint8_t* src, size_t n, fse_norm_histogram* out);
+/* NormHistogram::write (histogram.rs:376-431): appends the header at
+ * dst[*dst_len], advances *dst_len, *bits_written = the returned bit count. */
+int norm_histogram_write(const fse_norm_histogram* nh, uint8_t* dst, size_t dst_cap, size_t* dst_len,
+                         uint64_t* bits_written);
+/* NormHistogram::read (histogram.rs:436-505): *consumed = header bytes (the
+ * remaining slice starts there).  Errors: BAD_HEADER (TableLogTooLarge,
+ * TooManySymbols, UnexpectedEof), EMPTY. */
+int norm_histogram_read(const uint8_t* src, size_t n, fse_norm_histogram* out, size_t* consumed);
+/* EncodeTable::new / DecodeTable::new (fse.rs:88-189, 269-338). */
+int encode_table_new(const fse_norm_histogram* nh, fse_encode_table* out);
+int decode_table_new(const fse_norm_histogram* nh, fse_decode_table* out);
+/* fse_compress with its returned NormHistogram (lib.rs:112: the tuple's
+ * first element); otherwise as fse_compress. */
+int fse_compress_nh(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, size_t* dst_len,
+                    uint64_t* payload_bits, fse_norm_histogram* nh);
+
+/* The bitstream (bitstream/mod.rs:9-15).  A field is (value, width), width
+ * <= 32 (the crate's writer and readers take <= 16).
+ *  bitstack_write: BitStackWriter::new(dst) + write_bits_unmasked(vals[i],
+ *    nbits[i]) for each field + finish() (writer.rs:14-222): the fields
+ *    LSB-first from byte *dst_len on, zero-padded to a byte; appends,
+ *    advances *dst_len, *bits_written = finish()'s count.
+ *  bitstack_read: BitStackReader::new(src) (None -> NO_MARKER: empty or a
+ *    zero last byte, stack_reader.rs:17-92) + read(nbits[i]) per field
+ *    (top down); *n_read = reads that returned Some (the first None stops
+ *    them), *finished = finish() after them (stack_reader.rs:224-226).
+ *  bitstream_read: BitStreamReader::new(src, total_bits) (asserts
+ *    n == ceil(total_bits / 8) > 0 -> BAD_ARG) + read(nbits[i]) per field;
+ *    *n_read = reads that returned Ok, *bits_left = available() after them. */
+int bitstack_write(const uint32_t* vals, const uint8_t* nbits, size_t count, uint8_t* dst, size_t dst_cap,
+                   size_t* dst_len, uint64_t* bits_written);
+int bitstack_read(const uint8_t* src, size_t n, const uint8_t* nbits, size_t count, uint32_t* vals, size_t* n_read,
+                  int* finished);
+int bitstream_read(const uint8_t* src, size_t n, uint64_t total_bits, const uint8_t* nbits, size_t count,
+                   uint32_t* vals, size_t* n_read, uint64_t* bits_left);
+
+/* ------------------------------------------------------------------------
  * (2) Batched device entry points
  * ------------------------------------------------------------------------ */
 
 typedef struct {
-    uint32_t block_size;    /* bytes per block; multiple of 16 when >1 block; default 65536 */
+    uint32_t block_size;    /* bytes per block, <= 2^28 (u32 bit counts); multiple of 16 when >1 block; default 65536 */
     uint32_t table_log;     /* 0 = NormHistogram::new (optimal); else Histogram::normalize(L) */
     uint32_t ckpt_interval; /* steps between decode checkpoints (power of two; >= 8 for 2-state
                                pairs, >= 16 for 1-state symbols), 0 = none */
-    uint32_t max_table_log; /* upper bound on L used by the blocks (11 or 12); 0 = derive */
+    uint32_t max_table_log; /* upper bound on L used by the blocks (5..15; kernels exist for <= 11,
+                               12 and <= 15); 0 = derive (encode) / 12 (decode) */
     uint32_t nstates;       /* block format: 2 (or 0) = fse_compress2 (lib.rs:146), 1 = fse_compress (lib.rs:112) */
 } fsehip_params;
 
@@ -107,7 +202,8 @@ int fsehip_decompress_blocks(const fsehip_params* p, const uint8_t* d_in, uint64
 /* Decode tables, built once per block (NormHistogram::read + DecodeTable,
  * histogram.rs:436-505, fse.rs:280-338) for decode-only workloads (C3):
  * d_dtables holds fsehip_dtable_bytes(max_table_log) bytes per block (entry
- * u32 = nbBits | symbol << 8 | 4*newState << 16), d_dtinfo one int32 per
+ * u32 = nbBits | symbol << 8 | newState << 18 for max_table_log <= 12, and
+ * newState << 17 above), d_dtinfo one int32 per
  * block (header bytes | tableLog << 16, or a negative status). */
 uint64_t fsehip_dtable_bytes(uint32_t max_table_log);
 int fsehip_build_dtables(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
@@ -141,6 +237,22 @@ int fsehip_unpack_blocks(const uint8_t* d_stream, const uint64_t* d_offsets, con
  * stream for the distributed scatter (entropy_coders_amd/dist.py). */
 int fsehip_copy_blocks(const uint8_t* d_src, const uint64_t* d_src_offsets, const uint32_t* d_lens, uint32_t n_blocks,
                        uint8_t* d_dst, const uint64_t* d_dst_offsets, fsehip_stream_t stream);
+
+/* The bitstream as device passes over `count` fields (a prefix scan of the
+ * widths places every field; HBM-bound).
+ *  fsehip_bitstack_write: fields LSB-first from bit 0 of d_out; d_out must
+ *    hold 4 * ceil(total / 32) bytes (<= 4 * count) and be 4-byte aligned;
+ *    *d_total_bits = the bit count.
+ *  fsehip_bitstack_read / fsehip_bitstream_read: d_in readable up to
+ *    roundup(n_bytes, 4); d_result[0] = reads that succeed, [1] = 1 when
+ *    they consume every available bit, [2] = status (NO_MARKER for a stack
+ *    without its marker). */
+int fsehip_bitstack_write(const uint32_t* d_vals, const uint8_t* d_nbits, uint64_t count, uint8_t* d_out,
+                          uint64_t out_cap, uint64_t* d_total_bits, fsehip_stream_t stream);
+int fsehip_bitstack_read(const uint8_t* d_in, uint64_t n_bytes, const uint8_t* d_nbits, uint64_t count,
+                         uint32_t* d_vals, uint64_t* d_result, fsehip_stream_t stream);
+int fsehip_bitstream_read(const uint8_t* d_in, uint64_t n_bytes, uint64_t total_bits, const uint8_t* d_nbits,
+                          uint64_t count, uint32_t* d_vals, uint64_t* d_result, fsehip_stream_t stream);
 
 /* histogram::count per block: d_counts[b*256 + s], d_table_len[b]. */
 int fsehip_histogram_blocks(const uint8_t* d_src, uint64_t n_total, uint32_t block_size, uint32_t* d_counts,

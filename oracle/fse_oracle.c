@@ -514,12 +514,22 @@ int fo_build_dtable(const fo_norm* nh, fo_dtable* dt) {
  * ====================================================================== */
 
 /* Encoder::new_first_symbol, fse.rs:210-218 */
-static inline uint32_t enc_init(const fo_ctable* ct, uint8_t sym) {
+/* Encoder::new_first_symbol, fse.rs:210-218, with Rust release semantics:
+ * u32 wrapping arithmetic, the index formed as an i32 (wrapping add, fse.rs:
+ * 215) and converted to usize, then the bounds-checked table read.  At
+ * tableLog 15 the rounding constant 1 << 15 no longer covers the smallest
+ * state of a symbol with norm >= 2: the subtraction wraps and the index
+ * usually lands outside the table, where the reference panics (index out of
+ * bounds) -> FSE_ERR_ENCODER_INIT; a power-of-two norm can instead land on
+ * another symbol's state, which the reference then uses as is. */
+static inline int enc_init(const fo_ctable* ct, uint8_t sym, uint32_t* out) {
     uint32_t bits = ct->dnb[sym];
     uint32_t bits_out = (bits + (1u << 15)) >> 16;
     uint32_t value = (bits_out << 16) - bits;
-    int64_t idx = (int64_t)(value >> bits_out) + ct->dfs[sym];
-    return ct->st[(size_t)idx];
+    int32_t idx = (int32_t)((value >> bits_out) + (uint32_t)ct->dfs[sym]);
+    if (idx < 0 || (uint32_t)idx >= (1u << ct->log2)) return FSE_ERR_ENCODER_INIT;
+    *out = ct->st[idx];
+    return FSE_OK;
 }
 
 /* Encoder::encode_raw, fse.rs:227-239 */
@@ -559,13 +569,11 @@ static int compress2_body(const uint8_t* src, size_t n, const fo_norm* nh, uint8
     uint32_t e0, e1;
     size_t pairs; /* number of full pairs handled by the main loop */
     if (n & 1) { /* 155-160 */
-        e0 = enc_init(&ct, src[n - 1]);
-        e1 = enc_init(&ct, src[n - 2]);
+        if ((rc = enc_init(&ct, src[n - 1], &e0)) || (rc = enc_init(&ct, src[n - 2], &e1))) return rc;
         enc_step(&ct, &e0, src[n - 3], &w); /* n odd and >= 2, so n >= 3 */
         pairs = (n - 3) / 2;
     } else { /* 161-165 */
-        e0 = enc_init(&ct, src[n - 2]);
-        e1 = enc_init(&ct, src[n - 1]);
+        if ((rc = enc_init(&ct, src[n - 2], &e0)) || (rc = enc_init(&ct, src[n - 1], &e1))) return rc;
         pairs = n / 2 - 1;
     }
     for (size_t k = pairs; k-- > 0;) { /* 167-176 */
@@ -685,11 +693,10 @@ int fo_compress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* 
     bw_init(&w, dst, cap, hlen);
     uint32_t e;
     size_t pairs;
+    if ((rc = enc_init(&ct, src[n - 1], &e))) return rc;
     if (n & 1) { /* first chunk has one byte: init only (121-123) */
-        e = enc_init(&ct, src[n - 1]);
         pairs = (n - 1) / 2;
     } else { /* 121-126 */
-        e = enc_init(&ct, src[n - 1]);
         enc_step(&ct, &e, src[n - 2], &w);
         pairs = n / 2 - 1;
     }

@@ -18,7 +18,7 @@ STATUS = {
     0: "OK", -1: "EMPTY", -2: "TOO_SHORT", -3: "ALL_ZERO_SYMBOL0", -4: "SINGLE_SYMBOL",
     -5: "BAD_HEADER", -6: "NO_MARKER", -7: "DST_TOO_SMALL", -8: "TABLELOG_RANGE",
     -9: "CURSED", -10: "BAD_TABLE", -11: "BAD_ARG", -12: "HIP", -13: "LENGTH_MISMATCH",
-    -14: "UNSUPPORTED", -15: "NO_DEVICE",
+    -14: "UNSUPPORTED", -15: "NO_DEVICE", -16: "BAD_SIDECAR", -17: "ENCODER_INIT",
 }
 
 
@@ -177,6 +177,33 @@ def normalize(h: Hist, log2: int) -> tuple[Norm, bool]:
     slow = C.c_int(0)
     _check(lib().fo_normalize(C.byref(h), log2, C.byref(nh), C.byref(slow)))
     return nh, bool(slow.value)
+
+
+def norm_new(src) -> Norm:
+    """NormHistogram::new (histogram.rs:299-303)."""
+    a = _u8(src)
+    nh = Norm()
+    _check(lib().fo_norm_new(_ptr(a), len(a), C.byref(nh)))
+    return nh
+
+
+def ctable(nh: Norm):
+    """EncodeTable::new (fse.rs:88-189): (log2, stateTable, deltaNbBits[256],
+    deltaFindState[256], spread symbols)."""
+    ct = CTable()
+    _check(lib().fo_build_ctable(C.byref(nh), C.byref(ct)))
+    size = 1 << ct.log2
+    return (ct.log2, np.ctypeslib.as_array(ct.st)[:size].copy(), np.ctypeslib.as_array(ct.dnb).copy(),
+            np.ctypeslib.as_array(ct.dfs).copy(), np.ctypeslib.as_array(ct.spread)[:size].copy())
+
+
+def dtable_nh(nh: Norm):
+    """DecodeTable::new (fse.rs:269-338): (log2, new_state[], sym[], nb[])."""
+    dt = DTable()
+    _check(lib().fo_build_dtable(C.byref(nh), C.byref(dt)))
+    size = 1 << dt.log2
+    return (dt.log2, np.ctypeslib.as_array(dt.new_state)[:size].copy(),
+            np.ctypeslib.as_array(dt.sym)[:size].copy(), np.ctypeslib.as_array(dt.nb)[:size].copy())
 
 
 def header_write(nh: Norm) -> bytes:

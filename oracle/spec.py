@@ -375,11 +375,19 @@ class _Enc:
     """Encoder (fse.rs:196-251)."""
 
     def __init__(self, tab, first: int):
+        # new_first_symbol (fse.rs:210-218): u32 wrapping, the index an i32
+        # (wrapping add) turned usize, then a bounds-checked read that panics
+        # outside the table (reachable at tableLog 15)
         self.st, self.dnb, self.dfs = tab
         b = self.dnb[first]
         bo = ((b + (1 << 15)) & M32) >> 16
         v = ((bo << 16) - b) & M32
-        self.x = self.st[(v >> bo) + self.dfs[first]]
+        idx = ((v >> bo) + self.dfs[first]) & M32
+        if idx >= 1 << 31:
+            idx -= 1 << 32
+        if not 0 <= idx < len(self.st):
+            raise SpecError("ENCODER_INIT")
+        self.x = self.st[idx]
 
     def step(self, s: int, sink: BitSink):
         bo = ((self.dnb[s] + self.x) & M32) >> 16

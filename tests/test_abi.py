@@ -13,7 +13,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_header_declares_exports():
     src = open(os.path.join(ROOT, "include", "fsehip.h")).read()
     declared = set(re.findall(r"^\w[\w\s\*]*?\b(\w+)\(", src, flags=re.M))
-    declared = {d for d in declared if d.startswith(("fse", "histogram"))}
+    declared = {d for d in declared if d.startswith(("fse", "histogram", "norm_histogram", "encode_table",
+                                                     "decode_table", "bitstack", "bitstream"))}
     assert declared == set(_lib.EXPORTS), declared ^ set(_lib.EXPORTS)
 
 
@@ -42,3 +43,44 @@ def test_no_cpu_fallback_without_gpu():
     with pytest.raises(FseError) as e:
         compress2(b"abcabcabd" * 10)
     assert e.value.code == "NO_DEVICE"
+
+
+def test_pod_layouts():
+    """The plain-data twins of the Rust types have the C header's layout."""
+    import ctypes as C
+
+    assert C.sizeof(_lib.Histogram) == 256 * 4 + 8
+    assert C.sizeof(_lib.NormHistogram) == 256 * 4 + 8
+    assert C.sizeof(_lib.EncodeTable) == 4 + 2 * 32768 + 32768 + 256 * 8
+    assert C.sizeof(_lib.DecodeTransform) == 4
+    assert C.sizeof(_lib.DecodeTable) == 8 + 4 * 32768
+    assert _lib.EncodeTable.symbol_tt.offset == 4 + 2 * 32768 + 32768
+
+
+def test_block_size_limit_rejected_before_any_gpu_work():
+    """Blocks above 2^28 bytes would overflow the kernels' u32 bit counts:
+    both batched entry points refuse them (UNSUPPORTED) up front."""
+    import ctypes as C
+
+    lib = _lib.load()
+    p = _lib.Params(1 << 29, 0, 128, 11, 2)
+    fake = C.c_void_p(16)
+    rc = lib.fsehip_compress_blocks(C.byref(p), fake, 1 << 29, fake, 1 << 30, fake, fake, None, fake, None)
+    assert _lib.STATUS[rc] == "UNSUPPORTED"
+    rc = lib.fsehip_decompress_blocks(C.byref(p), fake, 1 << 30, fake, None, fake, 1 << 29, fake, None)
+    assert _lib.STATUS[rc] == "UNSUPPORTED"
+
+
+def test_building_blocks_fail_loudly_without_gpu():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from entropy_coders_amd import (FseError, bitstack_write, histogram_new, norm_histogram_new,
+                                    norm_histogram_read)
+
+    for call in (lambda: histogram_new(b"abc"), lambda: norm_histogram_new(b"abcabd"),
+                 lambda: norm_histogram_read(b"\x06\x10"), lambda: bitstack_write([1, 2], [3, 4])):
+        with pytest.raises(FseError) as e:
+            call()
+        assert e.value.code == "NO_DEVICE"

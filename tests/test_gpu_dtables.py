@@ -1,6 +1,6 @@
 """Decode tables on the GPU (fsehip_build_dtables, C3's pre-built dtables)
 against the oracle's DecodeTable (fse.rs:280-338), and the three decode
-routes (fused kernel, two-kernel default, pre-built tables) against the
+routes (segment-parallel, serial, pre-built tables) against the
 source."""
 import os
 
@@ -48,6 +48,10 @@ def test_dtables_match_oracle(torch_cuda, kind, prob, log2):
 
 
 def test_decode_routes_agree(torch_cuda):
+    """Every decode route gives the source back: segment-parallel with the
+    sidecar (tables built inside), serial without it, prebuilt tables with
+    and without the sidecar, and the sidecar recorded by the serial decoder
+    equal to the encoder's."""
     torch = torch_cuda
     from entropy_coders_amd import BlockCodec
 
@@ -55,33 +59,22 @@ def test_decode_routes_agree(torch_cuda):
     n = 48 * 65536 + 4321
     src = codec.generate(0, 0.2, 0x5EED0008, n)
     cb = codec.compress(src)
-    outs = {}
-    for name, env in (("fused4", {"FSEHIP_DEC_FUSED": "1", "FSEHIP_DEC_WAVES": "4", "FSEHIP_DEC_VAR": "2"}),
-                      ("fused8", {"FSEHIP_DEC_FUSED": "1", "FSEHIP_DEC_WAVES": "8", "FSEHIP_DEC_VAR": "2"}),
-                      ("two_kernel", {"FSEHIP_DEC_FUSED": "0", "FSEHIP_DEC_WAVES": "4", "FSEHIP_DEC_VAR": "2"}),
-                      ("two_kernel8", {"FSEHIP_DEC_FUSED": "0", "FSEHIP_DEC_WAVES": "8", "FSEHIP_DEC_VAR": "2"}),
-                      ("padded4", {"FSEHIP_DEC_FUSED": "0", "FSEHIP_DEC_WAVES": "4", "FSEHIP_DEC_VAR": "3"}),
-                      ("padded8", {"FSEHIP_DEC_FUSED": "0", "FSEHIP_DEC_WAVES": "8", "FSEHIP_DEC_VAR": "3"})):
-        old = {k: os.environ.get(k) for k in env}
-        os.environ.update(env)
-        try:
-            out, st = codec.decompress(cb)
-            torch.cuda.synchronize()
-        finally:
-            for k, v in old.items():
-                if v is None:
-                    os.environ.pop(k, None)
-                else:
-                    os.environ[k] = v
-        assert int(st.abs().max()) == 0, name
-        assert torch.equal(out, src), name
-        outs[name] = out
+    for side in (True, False):
+        out, st = codec.decompress(cb, use_sidecar=side)
+        torch.cuda.synchronize()
+        assert int(st.abs().max()) == 0 and torch.equal(out, src), side
     tabs = codec.build_dtables(cb)
-    out = torch.empty_like(src)
-    st = torch.zeros(codec.n_blocks(n), dtype=torch.int32, device=src.device)
-    codec.decompress_dt_into(cb, tabs, out, st)
+    for side in (True, False):
+        out = torch.empty_like(src)
+        st = torch.zeros(codec.n_blocks(n), dtype=torch.int32, device=src.device)
+        codec.decompress_dt_into(cb, tabs, out, st, use_sidecar=side)
+        torch.cuda.synchronize()
+        assert int(st.abs().max()) == 0 and torch.equal(out, src), side
+    out, side, st = codec.build_sidecar(cb)
     torch.cuda.synchronize()
     assert int(st.abs().max()) == 0 and torch.equal(out, src)
+    nb = codec.n_blocks(n)
+    assert torch.equal(side[: nb * codec.side_per_block], cb["sidecar"][: nb * codec.side_per_block])
 
 
 def test_dtables_error_blocks(torch_cuda):

@@ -35,19 +35,25 @@ def test_histogram_count(torch_cuda):
 def test_compress2_golden(torch_cuda, golden):
     from entropy_coders_amd import compress2, compress2_log, decompress2
 
+    from entropy_coders_amd import FseError
+
     manifest, arrays = golden
     for case in manifest["cases"]:
         if case["format"] != 2:
             continue
         src = arrays[case["name"] + "__src"]
+        run = (lambda: compress2(src)) if case["log2"] is None else (lambda: compress2_log(src, case["log2"]))
+        if "status" in case:  # the reference panics (new_first_symbol at tableLog 15)
+            with pytest.raises(FseError) as e:
+                run()
+            assert e.value.code == case["status"], case["name"]
+            continue
         want = arrays[case["name"] + "__comp"].tobytes()
-        if case["log2"] is None:
-            got, bits = compress2(src)
-        else:
-            got, bits = compress2_log(src, case["log2"])
+        got, bits = run()
         assert got == want, case["name"]
         assert bits == case["payload_bits"], case["name"]
-        assert decompress2(want) == src.tobytes(), case["name"]
+        if case.get("roundtrip", True):
+            assert decompress2(want) == src.tobytes(), case["name"]
 
 
 @pytest.mark.parametrize("n", [2, 3, 4, 5, 6, 7, 8, 9, 15, 16, 17, 31, 33, 63, 64, 65, 127, 255, 256,
