@@ -23,9 +23,11 @@ def main():
     d = sys.argv[1]
     vals = defaultdict(dict)
     for f in sorted(glob.glob(f"{d}/p*/**/*counter_collection.csv", recursive=True)):
+        seen = defaultdict(set)
         for r in csv.DictReader(open(f)):
             groups = int(r["Grid_Size"]) // max(int(r["Workgroup_Size"]), 1)
-            name = classify(r["Kernel_Name"], groups)
+            seen[r["Kernel_Name"]].add(int(r["Dispatch_Id"]))
+            name = classify(r["Kernel_Name"], groups, len(seen[r["Kernel_Name"]]) - 1)
             if not name:
                 continue
             vals[name][r["Counter_Name"]] = float(r["Counter_Value"])  # last launch wins
@@ -46,7 +48,8 @@ def main():
                     row[k.lower() + "_frac_of_wave_cycles"] = round(v[k] / wc, 4)
         if v.get("GRBM_GUI_ACTIVE") and "SQ_LDS_IDX_ACTIVE" in v:
             # LDS-array busy cycles per CU per GPU cycle (256 CUs)
-            row["lds_busy_per_cu_cycle"] = round(v["SQ_LDS_IDX_ACTIVE"] / (v["GRBM_GUI_ACTIVE"] * 256), 4)
+            # GRBM_GUI_ACTIVE sums the 8 XCDs: per-XCD cycles = / 8
+            row["lds_busy_per_cu_cycle"] = round(v["SQ_LDS_IDX_ACTIVE"] / (v["GRBM_GUI_ACTIVE"] / 8 * 256), 4)
         out[name] = row
         print(name, json.dumps({k: x for k, x in row.items() if not k.startswith("SQ_") and not k.startswith("GRBM")}))
     if "--json" in sys.argv:

@@ -17,8 +17,13 @@ import sys
 from collections import defaultdict
 
 
-def classify(kernel: str, groups: int):
+def classify(kernel: str, groups: int, nth: int = 0):
+    """Launch kind; `nth` = 0-based occurrence of this kernel name in the run
+    (the pipelined decode runs a fixed grid: tools/prof_bench.py launches it
+    twice on C2, then twice on C3)."""
     c3 = groups == 32768
+    if "decode_pipe_kernel" in kernel:
+        return "fse_decode_blocks" + ("_c3" if nth >= 2 else "")
     if "encode_blocks_kernel" in kernel:
         return "fse_encode_blocks" + ("_c3_input" if c3 else "")
     if "dtable_blocks_kernel" in kernel:
@@ -38,11 +43,13 @@ def classify(kernel: str, groups: int):
 def load(d, counter):
     vals = defaultdict(list)
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+        seen = defaultdict(set)
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
             groups = int(r["Grid_Size"]) // max(int(r["Workgroup_Size"]), 1)
-            name = classify(r["Kernel_Name"], groups)
+            seen[r["Kernel_Name"]].add(int(r["Dispatch_Id"]))
+            name = classify(r["Kernel_Name"], groups, len(seen[r["Kernel_Name"]]) - 1)
             if name:
                 vals[name].append(float(r["Counter_Value"]) * 1024.0)
     return vals
