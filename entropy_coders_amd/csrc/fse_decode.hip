@@ -592,10 +592,11 @@ __global__ __launch_bounds__(64) void decode1_serial_kernel(DecParams P) {
 // block never did, the rest after 25K-40K symbols), so speculative segment
 // decoding cannot replace the sidecar for this format.  The
 // serial decode is instead made as short a dependency chain as possible and
-// run at high occupancy: the block's prebuilt table sits in LDS (8 KiB ->
-// 20 blocks in flight per CU), one lane walks the stream (lib.rs:227-244)
-// and the bits come through a register window fed from 16-byte chunks
-// loaded a whole chunk ahead.
+// run at high occupancy.  This kernel serves tables above L = 12 (128 KiB
+// at L = 15): the block's prebuilt table sits in LDS, one lane walks the
+// stream (lib.rs:227-244) and the bits come through a register window fed
+// from 16-byte chunks loaded a chunk ahead.  At L <= 12 serial_ring_kernel
+// below replaces it (3x faster at C2).
 //   Container mode (n_total > 0): the raw length ends the block, as the
 //   oracle's decompress2 with a known length.
 //   Reference mode (n_total == 0, the host fse_decompress2): the block ends
@@ -759,6 +760,285 @@ __global__ __launch_bounds__(64) void serial2_decode_kernel(DecParams P) {
 }
 
 // ------------------------------------------------------------------------
+// Sidecar-less 2-state decode at L <= 12 (the serial decode above, made
+// 3x faster at C2).  Two things bound that kernel: its single lane is
+// provably lane 0, so the compiler runs the chain as wave-uniform SALU+VALU
+// code (~30 issue slots per pair for one chain), and its register window
+// waits on the global prefetch at every refill (the compiler merges the
+// prefetched registers at each refill branch, so it waits for the load,
+// and for any output store issued after it).  Here:
+//   - K blocks per workgroup, lane j of wave 0 walking block j: one VALU
+//     instruction advances K chains (K = 4 at L <= 11: 4 x (8 KiB table +
+//     1 KiB ring) = 36 KB, 4 workgroups = 16 chains per CU);
+//   - wave 1 streams each block's payload top down into its 256-word LDS
+//     ring in 256-byte chunks (one dword per lane), as far ahead as the ring
+//     allows, and publishes the lowest word landed (ctl[0]);
+//   - the decode lanes read only LDS (one payload word and the two table
+//     entries per pair, issued together, as the segment decoder's
+//     LdsChain), publish the highest word they may still read every 8 pairs
+//     (ctl[1]) and store their output without ever waiting on memory.
+// Same end checks, statuses and sidecar recording as serial2.
+// ------------------------------------------------------------------------
+constexpr uint32_t RING_WORDS = 256u, RING_MASK = RING_WORDS - 1u, RING_CHUNK = 64u;
+
+// Relaxed workgroup-scope atomics keep these as plain ds_read/ds_write (a
+// volatile access through a generic pointer becomes a FLAT access that
+// waits on vmcnt, i.e. on the output stores); the asm barriers pin their
+// place among the ring reads and writes, and LDS runs one wave's accesses
+// in order.
+__device__ __forceinline__ int32_t lds_load_volatile(int32_t* p) {
+    const int32_t v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __asm__ __volatile__("" ::: "memory");
+    return v;
+}
+__device__ __forceinline__ void lds_store_volatile(int32_t* p, int32_t v) {
+    __asm__ __volatile__("" ::: "memory");
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+struct RingChain {  // LdsChain over the ring
+    int32_t pos, B;
+    uint32_t whi, wlo, a0, a1;
+    __device__ __forceinline__ void init(const uint32_t* ring, int32_t p, uint32_t s0, uint32_t s1) {
+        pos = p;
+        a0 = s0 << 2;
+        a1 = s1 << 2;
+        B = (p - 24) & ~31;
+        wlo = 0;
+        whi = ring[((uint32_t)(B >> 5) + 1u) & RING_MASK];
+    }
+    __device__ __forceinline__ uint32_t pair(const uint32_t* ring, const uint8_t* dtb) {
+        const int32_t lo = (pos - 24) & ~31;
+        const uint32_t w0 = ring[(uint32_t)(lo >> 5) & RING_MASK];
+        const uint32_t e0 = *reinterpret_cast<const uint32_t*>(dtb + a0);
+        const uint32_t e1 = *reinterpret_cast<const uint32_t*>(dtb + a1);
+        const uint32_t w1 = lo == B ? whi : wlo;
+        pos -= (int32_t)((e0 + e1) & 0xFFu);
+        const uint32_t x = (uint32_t)((((uint64_t)w1 << 32) | w0) >> (uint32_t)(pos - lo));
+        B = lo;
+        whi = w1;
+        wlo = w0;
+        const uint32_t v1 = __builtin_amdgcn_ubfe(x, 0u, e1);
+        const uint32_t v0 = __builtin_amdgcn_ubfe(x, e1, e0);
+        a0 = (e0 >> 16) + (v0 << 2);
+        a1 = (e1 >> 16) + (v1 << 2);
+        return __builtin_amdgcn_perm(e1, e0, 0x0c0c0501u);  // sym0 | sym1 << 8
+    }
+};
+
+template <int LMAX, uint32_t K>
+__global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
+    static_assert(LMAX <= 12, "entry layout ns << 18: e >> 16 is the next entry's byte offset");
+    static_assert(K >= 1 && K <= 64, "one decode lane per block");
+    constexpr uint32_t TW = 1u << LMAX;
+    __shared__ __attribute__((aligned(16))) uint32_t tab_all[K * TW];
+    __shared__ uint32_t ring_all[K * RING_WORDS];
+    __shared__ int32_t ctl_all[K][2];  // [0] lowest word landed, [1] highest word the decoder may still read; INT32_MIN = stop
+    __shared__ uint32_t any_nb[K];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint64_t gb0 = (uint64_t)blockIdx.x * K;
+    if (tid < K) {
+        const uint64_t gb = gb0 + tid;
+        int32_t nw = 0;
+        if (gb < P.n_blocks && P.dtinfo[gb] >= 0) nw = (int32_t)((P.comp_len[gb] + 3u) >> 2);
+        ctl_all[tid][0] = nw;  // nothing landed yet
+        ctl_all[tid][1] = nw;
+        any_nb[tid] = 0;
+    }
+    __syncthreads();
+    for (uint32_t j = 0; j < K; ++j) {  // stage the prebuilt tables (dtable_blocks_kernel)
+        const uint64_t gb = gb0 + j;
+        if (gb >= P.n_blocks) break;
+        const int32_t info = P.dtinfo[gb];
+        if (info < 0) continue;
+        const uint32_t nv = (1u << ((uint32_t)info >> 16)) >> 2;
+        const uint4* t4 = reinterpret_cast<const uint4*>(P.dt + gb * (uint64_t)TW);
+        uint4* d4 = reinterpret_cast<uint4*>(tab_all + j * TW);
+        uint32_t nbor = 0;
+        for (uint32_t i = tid; i < nv; i += 128u) {
+            const uint4 q = t4[i];
+            d4[i] = q;
+            nbor |= (q.x | q.y | q.z | q.w) & 0xFFu;
+        }
+        if (nbor) atomicOr(&any_nb[j], 1u);
+    }
+    __syncthreads();
+
+    if (tid >= 64u) {  // wave 1: the loader, for all K rings (wave-uniform control)
+        int32_t k[K], nwj[K];
+        const uint32_t* wj[K];
+        uint32_t act = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < K; ++j) {
+            nwj[j] = ctl_all[j][1];
+            k[j] = (nwj[j] - 1) / (int32_t)RING_CHUNK;
+            wj[j] = reinterpret_cast<const uint32_t*>(P.in + (gb0 + j) * P.slot_bytes);
+            if (nwj[j] > 0) act |= 1u << j;
+        }
+        while (act) {
+            bool moved = false;
+#pragma unroll
+            for (uint32_t j = 0; j < K; ++j) {
+                if (!(act & (1u << j))) continue;
+                const int32_t need = lds_load_volatile(&ctl_all[j][1]);
+                if (need == INT32_MIN) {  // the decoder is done (or failed)
+                    act &= ~(1u << j);
+                    continue;
+                }
+                // chunk c may overwrite the slots of words 64c + RING_WORDS..: dead once above `need`
+                int32_t k1 = k[j];
+                while (k1 >= 0 && k1 > k[j] - (int32_t)(RING_WORDS / RING_CHUNK) &&
+                       k1 * (int32_t)RING_CHUNK + (int32_t)RING_WORDS > need)
+                    --k1;
+                if (k1 == k[j]) continue;
+                uint32_t v[RING_WORDS / RING_CHUNK];  // all loads in flight before the first LDS write
+#pragma unroll
+                for (int32_t q = 0; q < (int32_t)(RING_WORDS / RING_CHUNK); ++q) {
+                    const int32_t wi = (k[j] - q) * (int32_t)RING_CHUNK + (int32_t)lane;
+                    v[q] = (k[j] - q > k1 && wi < nwj[j]) ? wj[j][wi] : 0u;
+                }
+#pragma unroll
+                for (int32_t q = 0; q < (int32_t)(RING_WORDS / RING_CHUNK); ++q)
+                    if (k[j] - q > k1)
+                        ring_all[j * RING_WORDS +
+                                 ((uint32_t)((k[j] - q) * (int32_t)RING_CHUNK + (int32_t)lane) & RING_MASK)] = v[q];
+                k[j] = k1;
+                if (lane == 0) lds_store_volatile(&ctl_all[j][0], (k1 + 1) * (int32_t)RING_CHUNK);
+                if (k1 < 0) act &= ~(1u << j);
+                moved = true;
+            }
+            if (!moved) __builtin_amdgcn_s_sleep(2);
+        }
+        return;
+    }
+    const uint64_t gb = gb0 + lane;
+    if (lane >= K || gb >= P.n_blocks) return;
+
+    // wave 0, lane j < K: the decoder of block gb0 + j
+    uint32_t* const tab = tab_all + lane * TW;
+    const uint32_t* const ring = ring_all + lane * RING_WORDS;
+    int32_t* const ctl = ctl_all[lane];
+    const int32_t info = P.dtinfo[gb];
+    const uint8_t* in = P.in + gb * P.slot_bytes;
+    const uint32_t clen = info >= 0 ? P.comp_len[gb] : 0u;
+    const int32_t nw = (int32_t)((clen + 3u) >> 2);
+    const bool single = any_nb[lane] == 0u;
+    const bool known = P.n_total != 0;
+    const uint64_t ooff = gb * (uint64_t)P.block_size;
+    const uint32_t n = known ? (uint32_t)min((uint64_t)P.block_size, P.n_total - ooff) : 0u;
+    const uint32_t lim = known ? n : P.out_cap;
+    uint8_t* out = P.out + ooff;
+    int32_t err = info < 0 ? info : FSE_OK;
+    if (err == FSE_OK && known && n < 2) err = FSE_ERR_LENGTH_MISMATCH;
+    if (err == FSE_OK && !known && single) err = FSE_ERR_SINGLE_SYMBOL;
+    const int32_t hdr_bits = (info & 0xFFFF) * 8;
+    const uint32_t L = (uint32_t)info >> 16;
+    uint32_t o = 0;
+    int32_t top = 0;
+    if (err == FSE_OK) {
+        top = (int32_t)(clen - 1u) * 8 + (int32_t)ilog2u(in[clen - 1]);
+        if (top - 2 * (int32_t)L < hdr_bits) err = FSE_ERR_TOO_SHORT;
+    }
+    if (err == FSE_OK) {
+        const uint8_t* dtb = reinterpret_cast<const uint8_t*>(tab);
+        int32_t avail = nw;
+        auto wait_words = [&](int32_t wlow) {  // words >= max(wlow, 0) have landed
+            wlow = max(wlow, 0);
+            while (avail > wlow) {
+                avail = lds_load_volatile(&ctl[0]);
+                if (avail > wlow) __builtin_amdgcn_s_sleep(1);
+            }
+        };
+        // bits [p, p + 32) via the ring (end-of-block steps)
+        auto bits_at = [&](int32_t p) -> uint32_t {
+            const uint32_t wi = (uint32_t)p >> 5;
+            return __builtin_amdgcn_alignbit(ring[(wi + 1u) & RING_MASK], ring[wi & RING_MASK], (uint32_t)p);
+        };
+        wait_words((top - 2 * (int32_t)L) >> 5);
+        const uint32_t s0i = bits_at(top - (int32_t)L) & ((1u << L) - 1u);
+        const uint32_t s1i = bits_at(top - 2 * (int32_t)L) & ((1u << L) - 1u);
+        RingChain c;
+        c.init(ring, top - 2 * (int32_t)L, s0i, s1i);
+        const uint32_t I = P.ckpt_interval;
+        uint64_t* rec = (P.sidecar_out && I) ? P.sidecar_out + gb * P.ckpt_per_block : nullptr;
+        uint32_t pidx = 0, next_ck = rec && P.ckpt_per_block ? 0u : 0xFFFFFFFFu, ck = 0;
+        auto record_at = [&](int32_t p, uint32_t s0, uint32_t s1) {  // one compare per pair when idle
+            if (pidx == next_ck) {
+                rec[ck++] = (uint64_t)(uint32_t)(p - hdr_bits) | ((uint64_t)s0 << 32) | ((uint64_t)s1 << 48);
+                next_ck = ck < P.ckpt_per_block ? next_ck + I : 0xFFFFFFFFu;
+            }
+        };
+        auto record = [&]() { record_at(c.pos, c.a0 >> 2, c.a1 >> 2); };
+        // bulk: 8 pairs (<= 16L bits, 16 output bytes) without end checks
+        while (o + 18u < lim && c.pos - hdr_bits >= 16 * (int32_t)L) {
+            wait_words((c.pos - 24 - 16 * (int32_t)L) >> 5);
+            uint32_t w[4];
+#pragma unroll
+            for (uint32_t j = 0; j < 8u; j += 2u) {
+                record();
+                const uint32_t lo = c.pair(ring, dtb);
+                ++pidx;
+                record();
+                const uint32_t hi = c.pair(ring, dtb);
+                ++pidx;
+                w[j >> 1] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+            }
+            *reinterpret_cast<uint4*>(out + o) = make_uint4(w[0], w[1], w[2], w[3]);
+            o += 16;
+            lds_store_volatile(&ctl[1], (c.pos - 24) >> 5);
+        }
+        // the tail reads words <= pos/32 + 1, and it ends within 16L bits
+        // (bulk stopped by the position) or within 10 pairs (stopped by the
+        // output limit): wait for just those words, the loader cannot pass
+        // the ring's words above what the decoder still reads
+        lds_store_volatile(&ctl[1], (c.pos >> 5) + 1);
+        wait_words(max(hdr_bits, c.pos - 20 * (int32_t)L) >> 5);
+        // tail: pair by pair with the reference's end checks (lib.rs:227-244)
+        uint32_t s0 = c.a0 >> 2, s1 = c.a1 >> 2;
+        int32_t pos = c.pos;
+        auto pop = [&](uint32_t nb) -> uint32_t {
+            pos -= (int32_t)nb;
+            return bits_at(pos) & ((1u << nb) - 1u);
+        };
+        const int32_t full = known ? FSE_ERR_LENGTH_MISMATCH : FSE_ERR_DST_TOO_SMALL;
+        for (;; ++pidx) {
+            record_at(pos, s0, s1);
+            if (known && o + 2u >= n) {
+                if (o < n) out[o++] = (uint8_t)dte_sym(tab[s0]);
+                if (o < n) out[o++] = (uint8_t)dte_sym(tab[s1]);
+                break;
+            }
+            const uint32_t e0 = tab[s0];
+            uint32_t nb = dte_nb(e0);
+            if (pos - (int32_t)nb < hdr_bits) {  // decoder 0 cannot read: lib.rs:242-243
+                if (o + 2u > lim) { err = full; break; }
+                out[o++] = (uint8_t)dte_sym(e0);
+                out[o++] = (uint8_t)dte_sym(tab[s1]);
+                break;
+            }
+            s0 = Dte<LMAX>::ns(e0) + pop(nb);
+            if (o >= lim) { err = full; break; }
+            out[o++] = (uint8_t)dte_sym(e0);
+            const uint32_t e1 = tab[s1];
+            nb = dte_nb(e1);
+            if (pos - (int32_t)nb < hdr_bits) {  // decoder 1 cannot read: lib.rs:235-239
+                if (o + 2u > lim) { err = full; break; }
+                out[o++] = (uint8_t)dte_sym(e1);
+                out[o++] = (uint8_t)dte_sym(tab[s0]);
+                break;
+            }
+            s1 = Dte<LMAX>::ns(e1) + pop(nb);
+            if (o >= lim) { err = full; break; }
+            out[o++] = (uint8_t)dte_sym(e1);
+        }
+        if (err == FSE_OK && known && o != n) err = FSE_ERR_LENGTH_MISMATCH;
+    }
+    lds_store_volatile(&ctl[1], INT32_MIN);  // release the loader
+    P.status[gb] = err;
+    if (P.out_len) P.out_len[gb] = err ? 0u : o;
+}
+
+// ------------------------------------------------------------------------
 // launch wrappers
 // ------------------------------------------------------------------------
 hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) {
@@ -770,8 +1050,9 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
             else if (lmax <= 12) hipLaunchKernelGGL((decode1_serial_kernel<12>), g, dim3(64), 0, stream, P);
             else hipLaunchKernelGGL((decode1_serial_kernel<15>), g, dim3(64), 0, stream, P);
         } else {
-            if (lmax <= 11) hipLaunchKernelGGL((serial2_decode_kernel<11>), g, dim3(64), 0, stream, P);
-            else if (lmax <= 12) hipLaunchKernelGGL((serial2_decode_kernel<12>), g, dim3(64), 0, stream, P);
+            // 4 (L <= 11) or 2 (L = 12) blocks per workgroup: 16 / 8 chains per CU (LDS-bound)
+            if (lmax <= 11) hipLaunchKernelGGL((serial_ring_kernel<11, 4>), dim3((P.n_blocks + 3u) / 4u), dim3(128), 0, stream, P);
+            else if (lmax <= 12) hipLaunchKernelGGL((serial_ring_kernel<12, 2>), dim3((P.n_blocks + 1u) / 2u), dim3(128), 0, stream, P);
             else hipLaunchKernelGGL((serial2_decode_kernel<15>), g, dim3(64), 0, stream, P);
         }
         return hipGetLastError();

@@ -1,5 +1,7 @@
-"""Time the sidecar-less decode of C2 blocks (serial reference mode, one
-lane per block) on a reduced size.  Diagnostics for SURVEY 8(f3)."""
+"""Time the sidecar-less decode against the sidecar decode on
+a reduced size, for a few distributions and table logs; every result is
+checked against the source.  FSEHIP_SERIAL_OLD=1 selects the previous
+register-window serial kernel for A/B runs."""
 import os
 import sys
 import time
@@ -11,17 +13,32 @@ import torch  # noqa: E402
 from entropy_coders_amd import BlockCodec  # noqa: E402
 
 n = int(os.environ.get("NS_BYTES", 256 << 20))
-codec = BlockCodec(ckpt_interval=128)
-src = codec.generate(0, 0.155, 0x5EED0002, n)
-cb = codec.compress(src)
-out = torch.empty(n, dtype=torch.uint8, device="cuda")
-st = torch.zeros(codec.n_blocks(n), dtype=torch.int32, device="cuda")
-for use in (True, False):
-    codec.decompress_into(cb, out, st, use_sidecar=use)
+# (name, generator kind, prob, table_log): C2, uniform C5 L=11, skewed L=12
+cases = [("c2_lut0155", 0, 0.155, 0), ("uniform_L11", 1, 0.0, 11), ("lut077_L12", 0, 0.77, 12)]
+only = os.environ.get("NS_CASES")
+for name, kind, prob, tl in cases:
+    if only and name not in only.split(","):
+        continue
+    codec = BlockCodec(ckpt_interval=128, table_log=tl)
+    src = codec.generate(kind, prob, 0x5EED0002, n)
+    cb = codec.compress(src)
+    out = torch.empty(n, dtype=torch.uint8, device="cuda")
+    st = torch.zeros(codec.n_blocks(n), dtype=torch.int32, device="cuda")
+    res = {}
+    for use in (True, False):
+        codec.decompress_into(cb, out, st, use_sidecar=use)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        codec.decompress_into(cb, out, st, use_sidecar=use)
+        torch.cuda.synchronize()
+        t = time.perf_counter() - t0
+        ok = bool(torch.equal(out, src)) and int(st.abs().max()) == 0
+        res[use] = (t, ok)
+        out.fill_(0)
+    o2, side2, st2 = codec.build_sidecar(cb)
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    codec.decompress_into(cb, out, st, use_sidecar=use)
-    torch.cuda.synchronize()
-    t = time.perf_counter() - t0
-    ok = bool(torch.equal(out, src)) and int(st.abs().max()) == 0
-    print(f"sidecar={use}: {t * 1e3:.2f} ms for {n >> 20} MiB ({n / t / 2**30:.1f} GiB/s) ok={ok}", flush=True)
+    side_ok = bool(torch.equal(o2, src)) and int(st2.abs().max()) == 0 and bool(torch.equal(side2, cb["sidecar"]))
+    ratio = int(cb["comp_len"].sum()) / n
+    print(f"{name}: ratio {ratio:.3f}  sidecar {res[True][0] * 1e3:.2f} ms ({n / res[True][0] / 2**30:.0f} GiB/s, "
+          f"ok={res[True][1]})  no sidecar {res[False][0] * 1e3:.2f} ms ({n / res[False][0] / 2**30:.1f} GiB/s, "
+          f"ok={res[False][1]})  build_sidecar ok={side_ok}", flush=True)
