@@ -56,6 +56,7 @@ def parse():
     ap.add_argument("--no-c3", action="store_true", help="skip the decode-only (prebuilt tables) line")
     ap.add_argument("--c3-blocks", type=int, default=32768,
                     help="C3 size: blocks of C2 data (32768 x 64 KiB ~ 1 GiB compressed, SURVEY 8(d))")
+    ap.add_argument("--no-serial", action="store_true", help="skip the sidecar-less decode line")
     ap.add_argument("--no-sweep", action="store_true", help="skip the C5 distribution / table-log sweep")
     ap.add_argument("--sweep-bytes", type=int, default=256 << 20, help="raw bytes per C5 sweep point")
     ap.add_argument("--host", action="store_true",
@@ -382,6 +383,29 @@ def main():
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         ok = bool(flag.item())
 
+    # the same blocks decoded without their sidecar (the format the
+    # CPU crate writes): serial per block, several blocks per workgroup
+    serial = None
+    if not args.no_serial and world == 1 and args.nstates == 2:
+        codec.decompress_into(cb, out, dstat, use_sidecar=False)  # warm-up
+        out.fill_(0xA5)
+        dstat.fill_(-99)
+        torch.cuda.synchronize(dev)
+        es = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        reps = 2
+        es[0].record(stream)
+        for _ in range(reps):
+            codec.decompress_into(cb, out, dstat, use_sidecar=False)
+        es[1].record(stream)
+        torch.cuda.synchronize(dev)
+        s_ms = es[0].elapsed_time(es[1]) / reps
+        s_ok = int(dstat.abs().max()) == 0 and bool(torch.equal(out, src))
+        serial = {"workload": "the step's compressed blocks decoded without the sidecar (decode tables + "
+                              "serial_ring_kernel), HIP events",
+                  "decode_ms": round(s_ms, 4), "decode_GiB_s": round(n / (s_ms * 1e-3) / 2**30, 2),
+                  "verified": s_ok}
+        ok = ok and s_ok
+
     # C3 (BASELINE configs[2]): decode only, decode tables prebuilt and untimed,
     # on its own 32768 blocks of C2 data (~1 GiB compressed)
     c3 = None
@@ -484,6 +508,8 @@ def main():
             line["roofline"], line["roofline_decode"] = line["roofline_decode"], line["roofline"]
         if c3 is not None:
             line["c3_decode_only"] = c3
+        if serial is not None:
+            line["sidecar_less_decode"] = serial
         if gather_info is not None:
             line["c4_exchange"] = gather_info
         if host_info is not None:

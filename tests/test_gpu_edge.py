@@ -183,3 +183,27 @@ def test_corrupt_blocks_fail_cleanly(torch_cuda, use_sidecar):
             assert status[b] == 0 and torch.equal(buf[b * block:(b + 1) * block], src[b * block:(b + 1) * block])
     for b in (3, 4, 9, 10):  # truncated / marker cleared: always detected
         assert status[b] != 0, (b, status)
+
+
+@pytest.mark.parametrize("table_log,n_blocks", [(0, 1), (0, 3), (0, 5), (11, 7), (12, 1), (12, 3)])
+def test_sidecar_less_partial_groups(torch_cuda, table_log, n_blocks):
+    """The sidecar-less decoder packs K blocks into one workgroup (4 at
+    L <= 11, 2 at L = 12), one decode lane each: block counts that leave a
+    group part-empty, and a ragged last block, must decode exactly and
+    rebuild the encoder's sidecar."""
+    torch = torch_cuda
+    from entropy_coders_amd import BlockCodec
+
+    block = 65536
+    codec = BlockCodec(block_size=block, table_log=table_log, ckpt_interval=128)
+    n = n_blocks * block - 777
+    src = codec.generate(0, 0.155, 0x5EED0A00 + n_blocks, n)
+    cb = codec.compress(src)
+    out = torch.full((n,), 0xA5, dtype=torch.uint8, device=codec.device)
+    st = torch.full((n_blocks,), -99, dtype=torch.int32, device=codec.device)
+    codec.decompress_into(cb, out, st, use_sidecar=False)
+    o2, side2, st2 = codec.build_sidecar(cb)
+    torch.cuda.synchronize()
+    assert int(st.abs().max()) == 0 and int(st2.abs().max()) == 0
+    assert torch.equal(out, src) and torch.equal(o2, src)
+    assert torch.equal(side2, cb["sidecar"])

@@ -32,7 +32,7 @@ def classify(kernel: str, groups: int, nth: int = 0):
         if "67584u" in kernel:
             return "fse_decode_deferred" + ("_c3" if c3 else "")
         return "fse_decode_blocks" + ("_c3" if c3 else "")
-    for k, name in (("serial2_decode_kernel", "fse_decode_serial2"), ("decode_blocks_kernel", "fse_decode_fused"),
+    for k, name in (("serial_ring_kernel", "fse_decode_serial"), ("serial2_decode_kernel", "fse_decode_serial2"), ("decode_blocks_kernel", "fse_decode_fused"),
                     ("decode1_serial_kernel", "fse_decode1_serial"), ("pack_blocks_kernel", "fse_pack_blocks"),
                     ("copy_blocks_kernel", "fse_copy_blocks"), ("generate_kernel", "fse_generate")):
         if k in kernel:

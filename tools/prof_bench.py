@@ -3,6 +3,7 @@ the bench's kernels on the bench's data, each launch twice (the summary takes
 the last launch of each kind; the first may see a cold cache).
 
   C2: 16384 x 64 KiB (LUT p=0.155): encode, decode tables, decode
+  C2 again without the sidecar: the serial (sidecar-less) decode
   C3: 32768 x 64 KiB of the same distribution: decode with prebuilt tables
 
 The summariser (tools/pmc_summary.py) tells the launches apart by kernel
@@ -28,6 +29,12 @@ for _ in range(2):
     codec.decompress_into(cb, out, st)
 torch.cuda.synchronize()
 assert torch.equal(out, src)
+if not int(os.environ.get("PROF_NO_SERIAL", 0)):  # sidecar-less decode (serial_ring_kernel)
+    for _ in range(2):
+        out.fill_(0)
+        codec.decompress_into(cb, out, st, use_sidecar=False)
+    torch.cuda.synchronize()
+    assert torch.equal(out, src)
 del out
 if not int(os.environ.get("PROF_NO_C3", 0)):
     n3 = 32768 * 65536
