@@ -339,7 +339,7 @@ static int decompress_impl(const fsehip_params* p, const uint8_t* d_in, uint64_t
     if ((d_sidecar || d_sidecar_out) &&
         (p->ckpt_interval < (ns == 1 ? 16u : 8u) || (p->ckpt_interval & (p->ckpt_interval - 1))))
         return FSE_ERR_BAD_ARG;
-    if (ns == 1 && d_sidecar_out) return FSE_ERR_UNSUPPORTED;  // the recorder is the 2-state serial decoder
+    if (ns == 1 && d_sidecar_out && kern_lmax(p->max_table_log) > 12) return FSE_ERR_UNSUPPORTED;  // decode1_serial_kernel records nothing
     if (!device_ok()) return FSE_ERR_NO_DEVICE;
     fsehip::DecParams P{};
     P.nstates = ns;
@@ -432,8 +432,10 @@ int fsehip_build_sidecar(const fsehip_params* p, const uint8_t* d_in, uint64_t s
                          int32_t* d_status, fsehip_stream_t stream) {
     if (n_total == 0) return FSE_ERR_EMPTY;
     if (!p || !d_sidecar_out) return FSE_ERR_BAD_ARG;
-    if (p->nstates == 1) return FSE_ERR_UNSUPPORTED;
-    if (p->ckpt_interval < 8 || (p->ckpt_interval & (p->ckpt_interval - 1))) return FSE_ERR_BAD_ARG;
+    const uint32_t ns = p->nstates == 1 ? 1u : 2u;
+    // 1-state blocks above L = 12 decode on decode1_serial_kernel, which records nothing
+    if (ns == 1 && kern_lmax(p->max_table_log) > 12) return FSE_ERR_UNSUPPORTED;
+    if (p->ckpt_interval < (ns == 1 ? 16u : 8u) || (p->ckpt_interval & (p->ckpt_interval - 1))) return FSE_ERR_BAD_ARG;
     return with_dtables(p, d_in, slot_bytes, d_comp_len, n_total, stream, [&](const uint32_t* dt, const int32_t* info) {
         return decompress_impl(p, d_in, slot_bytes, d_comp_len, nullptr, d_out, n_total, d_sidecar_out, d_status,
                                nullptr, 0, stream, dt, info);

@@ -796,19 +796,25 @@ __device__ __forceinline__ void lds_store_volatile(int32_t* p, int32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-struct RingChain {  // LdsChain over the ring
+// LdsChain over the ring.  NS = 2: a pair (<= 24 bits) per step; NS = 1:
+// one symbol (<= 12 bits).  The window [lo, lo + 64) covers the step's bits
+// and lo moves down by at most one word per step, so the upper word is
+// either the previous upper word or the previous lower one.
+template <int NS>
+struct RingChain {
+    static constexpr int32_t OFF = 12 * NS;
     int32_t pos, B;
     uint32_t whi, wlo, a0, a1;
     __device__ __forceinline__ void init(const uint32_t* ring, int32_t p, uint32_t s0, uint32_t s1) {
         pos = p;
         a0 = s0 << 2;
         a1 = s1 << 2;
-        B = (p - 24) & ~31;
+        B = (p - OFF) & ~31;
         wlo = 0;
         whi = ring[((uint32_t)(B >> 5) + 1u) & RING_MASK];
     }
     __device__ __forceinline__ uint32_t pair(const uint32_t* ring, const uint8_t* dtb) {
-        const int32_t lo = (pos - 24) & ~31;
+        const int32_t lo = (pos - OFF) & ~31;
         const uint32_t w0 = ring[(uint32_t)(lo >> 5) & RING_MASK];
         const uint32_t e0 = *reinterpret_cast<const uint32_t*>(dtb + a0);
         const uint32_t e1 = *reinterpret_cast<const uint32_t*>(dtb + a1);
@@ -824,9 +830,23 @@ struct RingChain {  // LdsChain over the ring
         a1 = (e1 >> 16) + (v1 << 2);
         return __builtin_amdgcn_perm(e1, e0, 0x0c0c0501u);  // sym0 | sym1 << 8
     }
+    // NS = 1: one symbol; returns its entry (symbol in bits 8-15)
+    __device__ __forceinline__ uint32_t step(const uint32_t* ring, const uint8_t* dtb) {
+        const int32_t lo = (pos - OFF) & ~31;
+        const uint32_t w0 = ring[(uint32_t)(lo >> 5) & RING_MASK];
+        const uint32_t e = *reinterpret_cast<const uint32_t*>(dtb + a0);
+        const uint32_t w1 = lo == B ? whi : wlo;
+        pos -= (int32_t)(e & 0xFFu);
+        const uint32_t x = (uint32_t)((((uint64_t)w1 << 32) | w0) >> (uint32_t)(pos - lo));
+        B = lo;
+        whi = w1;
+        wlo = w0;
+        a0 = (e >> 16) + (__builtin_amdgcn_ubfe(x, 0u, e) << 2);
+        return e;
+    }
 };
 
-template <int LMAX, uint32_t K>
+template <int LMAX, uint32_t K, int NS>
 __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
     static_assert(LMAX <= 12, "entry layout ns << 18: e >> 16 is the next entry's byte offset");
     static_assert(K >= 1 && K <= 64, "one decode lane per block");
@@ -929,15 +949,17 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
     const uint32_t lim = known ? n : P.out_cap;
     uint8_t* out = P.out + ooff;
     int32_t err = info < 0 ? info : FSE_OK;
-    if (err == FSE_OK && known && n < 2) err = FSE_ERR_LENGTH_MISMATCH;
-    if (err == FSE_OK && !known && single) err = FSE_ERR_SINGLE_SYMBOL;
+    if (NS == 2 && err == FSE_OK && known && n < 2) err = FSE_ERR_LENGTH_MISMATCH;
+    // 2-state: a single-symbol table never ends in the reference (refused up
+    // front); 1-state: as decode1_serial_kernel, at the capacity
+    if (NS == 2 && err == FSE_OK && !known && single) err = FSE_ERR_SINGLE_SYMBOL;
     const int32_t hdr_bits = (info & 0xFFFF) * 8;
     const uint32_t L = (uint32_t)info >> 16;
     uint32_t o = 0;
     int32_t top = 0;
     if (err == FSE_OK) {
-        top = (int32_t)(clen - 1u) * 8 + (int32_t)ilog2u(in[clen - 1]);
-        if (top - 2 * (int32_t)L < hdr_bits) err = FSE_ERR_TOO_SHORT;
+        top = (int32_t)(clen - 1u) * 8 + (int32_t)ilog2u(in[clen - 1]);  // marker (BitStackReader::new)
+        if (top - NS * (int32_t)L < hdr_bits) err = FSE_ERR_TOO_SHORT;  // lib.rs:197 / 224-225 unwrap
     }
     if (err == FSE_OK) {
         const uint8_t* dtb = reinterpret_cast<const uint8_t*>(tab);
@@ -954,84 +976,123 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
             const uint32_t wi = (uint32_t)p >> 5;
             return __builtin_amdgcn_alignbit(ring[(wi + 1u) & RING_MASK], ring[wi & RING_MASK], (uint32_t)p);
         };
-        wait_words((top - 2 * (int32_t)L) >> 5);
+        wait_words((top - NS * (int32_t)L) >> 5);
         const uint32_t s0i = bits_at(top - (int32_t)L) & ((1u << L) - 1u);
-        const uint32_t s1i = bits_at(top - 2 * (int32_t)L) & ((1u << L) - 1u);
-        RingChain c;
-        c.init(ring, top - 2 * (int32_t)L, s0i, s1i);
+        const uint32_t s1i = NS == 2 ? bits_at(top - 2 * (int32_t)L) & ((1u << L) - 1u) : 0u;
+        RingChain<NS> c;
+        c.init(ring, top - NS * (int32_t)L, s0i, s1i);
         const uint32_t I = P.ckpt_interval;
         uint64_t* rec = (P.sidecar_out && I) ? P.sidecar_out + gb * P.ckpt_per_block : nullptr;
+        // checkpoint before pair (NS = 2) / symbol (NS = 1) pidx: bit position
+        // and the states, as the encoder records them
         uint32_t pidx = 0, next_ck = rec && P.ckpt_per_block ? 0u : 0xFFFFFFFFu, ck = 0;
-        auto record_at = [&](int32_t p, uint32_t s0, uint32_t s1) {  // one compare per pair when idle
+        auto record_at = [&](int32_t p, uint32_t s0, uint32_t s1) {  // one compare per step when idle
             if (pidx == next_ck) {
-                rec[ck++] = (uint64_t)(uint32_t)(p - hdr_bits) | ((uint64_t)s0 << 32) | ((uint64_t)s1 << 48);
+                rec[ck++] = (uint64_t)(uint32_t)(p - hdr_bits) | ((uint64_t)s0 << 32) |
+                            (NS == 2 ? (uint64_t)s1 << 48 : 0ull);
                 next_ck = ck < P.ckpt_per_block ? next_ck + I : 0xFFFFFFFFu;
             }
         };
         auto record = [&]() { record_at(c.pos, c.a0 >> 2, c.a1 >> 2); };
-        // bulk: 8 pairs (<= 16L bits, 16 output bytes) without end checks
+        // bulk: 16 output bytes (8 pairs / 16 symbols, <= 16L bits) without end checks
         while (o + 18u < lim && c.pos - hdr_bits >= 16 * (int32_t)L) {
-            wait_words((c.pos - 24 - 16 * (int32_t)L) >> 5);
+            wait_words((c.pos - NS * 12 - 16 * (int32_t)L) >> 5);
             uint32_t w[4];
+            if constexpr (NS == 2) {
 #pragma unroll
-            for (uint32_t j = 0; j < 8u; j += 2u) {
-                record();
-                const uint32_t lo = c.pair(ring, dtb);
-                ++pidx;
-                record();
-                const uint32_t hi = c.pair(ring, dtb);
-                ++pidx;
-                w[j >> 1] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+                for (uint32_t j = 0; j < 8u; j += 2u) {
+                    record();
+                    const uint32_t lo = c.pair(ring, dtb);
+                    ++pidx;
+                    record();
+                    const uint32_t hi = c.pair(ring, dtb);
+                    ++pidx;
+                    w[j >> 1] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+                }
+            } else {
+#pragma unroll
+                for (uint32_t j = 0; j < 4u; ++j) {
+                    uint32_t e[4];
+#pragma unroll
+                    for (uint32_t q = 0; q < 4u; ++q) {
+                        record();
+                        e[q] = c.step(ring, dtb);
+                        ++pidx;
+                    }
+                    w[j] = __builtin_amdgcn_perm(__builtin_amdgcn_perm(e[3], e[2], 0x0c0c0501u),
+                                                 __builtin_amdgcn_perm(e[1], e[0], 0x0c0c0501u), 0x05040100u);
+                }
             }
             *reinterpret_cast<uint4*>(out + o) = make_uint4(w[0], w[1], w[2], w[3]);
             o += 16;
-            lds_store_volatile(&ctl[1], (c.pos - 24) >> 5);
+            lds_store_volatile(&ctl[1], (c.pos - NS * 12) >> 5);
         }
         // the tail reads words <= pos/32 + 1, and it ends within 16L bits
-        // (bulk stopped by the position) or within 10 pairs (stopped by the
+        // (bulk stopped by the position) or within 18 steps (stopped by the
         // output limit): wait for just those words, the loader cannot pass
         // the ring's words above what the decoder still reads
         lds_store_volatile(&ctl[1], (c.pos >> 5) + 1);
         wait_words(max(hdr_bits, c.pos - 20 * (int32_t)L) >> 5);
-        // tail: pair by pair with the reference's end checks (lib.rs:227-244)
         uint32_t s0 = c.a0 >> 2, s1 = c.a1 >> 2;
         int32_t pos = c.pos;
         auto pop = [&](uint32_t nb) -> uint32_t {
             pos -= (int32_t)nb;
             return bits_at(pos) & ((1u << nb) - 1u);
         };
-        const int32_t full = known ? FSE_ERR_LENGTH_MISMATCH : FSE_ERR_DST_TOO_SMALL;
-        for (;; ++pidx) {
-            record_at(pos, s0, s1);
-            if (known && o + 2u >= n) {
-                if (o < n) out[o++] = (uint8_t)dte_sym(tab[s0]);
-                if (o < n) out[o++] = (uint8_t)dte_sym(tab[s1]);
-                break;
-            }
-            const uint32_t e0 = tab[s0];
-            uint32_t nb = dte_nb(e0);
-            if (pos - (int32_t)nb < hdr_bits) {  // decoder 0 cannot read: lib.rs:242-243
-                if (o + 2u > lim) { err = full; break; }
+        if constexpr (NS == 2) {
+            // tail: pair by pair with the reference's end checks (lib.rs:227-244)
+            const int32_t full = known ? FSE_ERR_LENGTH_MISMATCH : FSE_ERR_DST_TOO_SMALL;
+            for (;; ++pidx) {
+                record_at(pos, s0, s1);
+                if (known && o + 2u >= n) {
+                    if (o < n) out[o++] = (uint8_t)dte_sym(tab[s0]);
+                    if (o < n) out[o++] = (uint8_t)dte_sym(tab[s1]);
+                    break;
+                }
+                const uint32_t e0 = tab[s0];
+                uint32_t nb = dte_nb(e0);
+                if (pos - (int32_t)nb < hdr_bits) {  // decoder 0 cannot read: lib.rs:242-243
+                    if (o + 2u > lim) { err = full; break; }
+                    out[o++] = (uint8_t)dte_sym(e0);
+                    out[o++] = (uint8_t)dte_sym(tab[s1]);
+                    break;
+                }
+                s0 = Dte<LMAX>::ns(e0) + pop(nb);
+                if (o >= lim) { err = full; break; }
                 out[o++] = (uint8_t)dte_sym(e0);
-                out[o++] = (uint8_t)dte_sym(tab[s1]);
-                break;
-            }
-            s0 = Dte<LMAX>::ns(e0) + pop(nb);
-            if (o >= lim) { err = full; break; }
-            out[o++] = (uint8_t)dte_sym(e0);
-            const uint32_t e1 = tab[s1];
-            nb = dte_nb(e1);
-            if (pos - (int32_t)nb < hdr_bits) {  // decoder 1 cannot read: lib.rs:235-239
-                if (o + 2u > lim) { err = full; break; }
+                const uint32_t e1 = tab[s1];
+                nb = dte_nb(e1);
+                if (pos - (int32_t)nb < hdr_bits) {  // decoder 1 cannot read: lib.rs:235-239
+                    if (o + 2u > lim) { err = full; break; }
+                    out[o++] = (uint8_t)dte_sym(e1);
+                    out[o++] = (uint8_t)dte_sym(tab[s0]);
+                    break;
+                }
+                s1 = Dte<LMAX>::ns(e1) + pop(nb);
+                if (o >= lim) { err = full; break; }
                 out[o++] = (uint8_t)dte_sym(e1);
-                out[o++] = (uint8_t)dte_sym(tab[s0]);
-                break;
             }
-            s1 = Dte<LMAX>::ns(e1) + pop(nb);
-            if (o >= lim) { err = full; break; }
-            out[o++] = (uint8_t)dte_sym(e1);
+            if (err == FSE_OK && known && o != n) err = FSE_ERR_LENGTH_MISMATCH;
+        } else {
+            // tail: symbol by symbol (lib.rs:198-208), then Decoder::finish
+            for (;; ++pidx) {
+                record_at(pos, s0, 0u);
+                const uint32_t e = tab[s0];
+                const uint32_t nb = dte_nb(e);
+                if (pos - (int32_t)nb < hdr_bits) break;  // decode_symbol -> None
+                if (o >= lim) {  // nb == 0 forever: a probability-1 symbol never ends in the reference
+                    err = nb == 0 ? FSE_ERR_SINGLE_SYMBOL : FSE_ERR_DST_TOO_SMALL;
+                    break;
+                }
+                s0 = Dte<LMAX>::ns(e) + pop(nb);
+                out[o++] = (uint8_t)dte_sym(e);
+            }
+            if (err == FSE_OK) {
+                if (o >= lim) err = FSE_ERR_DST_TOO_SMALL;
+                else out[o++] = (uint8_t)dte_sym(tab[s0]);  // Decoder::finish (lib.rs:208)
+            }
+            if (known && (err == FSE_ERR_DST_TOO_SMALL || (err == FSE_OK && o != n))) err = FSE_ERR_LENGTH_MISMATCH;
         }
-        if (err == FSE_OK && known && o != n) err = FSE_ERR_LENGTH_MISMATCH;
     }
     lds_store_volatile(&ctl[1], INT32_MIN);  // release the loader
     P.status[gb] = err;
@@ -1046,13 +1107,13 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
     if (!P.dt || !P.dtinfo) return hipErrorInvalidValue;
     if (!P.sidecar) {  // serial: sidecar-less blocks, reference-mode host streams, sidecar recording
         if (P.nstates == 1) {
-            if (lmax <= 11) hipLaunchKernelGGL((decode1_serial_kernel<11>), g, dim3(64), 0, stream, P);
-            else if (lmax <= 12) hipLaunchKernelGGL((decode1_serial_kernel<12>), g, dim3(64), 0, stream, P);
+            if (lmax <= 11) hipLaunchKernelGGL((serial_ring_kernel<11, 4, 1>), dim3((P.n_blocks + 3u) / 4u), dim3(128), 0, stream, P);
+            else if (lmax <= 12) hipLaunchKernelGGL((serial_ring_kernel<12, 2, 1>), dim3((P.n_blocks + 1u) / 2u), dim3(128), 0, stream, P);
             else hipLaunchKernelGGL((decode1_serial_kernel<15>), g, dim3(64), 0, stream, P);
         } else {
             // 4 (L <= 11) or 2 (L = 12) blocks per workgroup: 16 / 8 chains per CU (LDS-bound)
-            if (lmax <= 11) hipLaunchKernelGGL((serial_ring_kernel<11, 4>), dim3((P.n_blocks + 3u) / 4u), dim3(128), 0, stream, P);
-            else if (lmax <= 12) hipLaunchKernelGGL((serial_ring_kernel<12, 2>), dim3((P.n_blocks + 1u) / 2u), dim3(128), 0, stream, P);
+            if (lmax <= 11) hipLaunchKernelGGL((serial_ring_kernel<11, 4, 2>), dim3((P.n_blocks + 3u) / 4u), dim3(128), 0, stream, P);
+            else if (lmax <= 12) hipLaunchKernelGGL((serial_ring_kernel<12, 2, 2>), dim3((P.n_blocks + 1u) / 2u), dim3(128), 0, stream, P);
             else hipLaunchKernelGGL((serial2_decode_kernel<15>), g, dim3(64), 0, stream, P);
         }
         return hipGetLastError();

@@ -218,7 +218,8 @@ int fsehip_decompress_blocks_dt(const fsehip_params* p, const uint8_t* d_in, uin
                                 fsehip_stream_t stream);
 
 /* Serial decode that also records the sidecar index (for streams produced
- * elsewhere, e.g. by the CPU crate), so later decodes run in parallel. */
+ * elsewhere, e.g. by the CPU crate), so later decodes run in parallel.
+ * 1-state blocks: table logs <= 12 (UNSUPPORTED above). */
 int fsehip_build_sidecar(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
                          const uint32_t* d_comp_len, uint8_t* d_out, uint64_t n_total, uint64_t* d_sidecar_out,
                          int32_t* d_status, fsehip_stream_t stream);

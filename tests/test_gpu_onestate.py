@@ -124,13 +124,18 @@ def _batched(torch, kind, prob, n_total, block=65536, seed=0x5EED1001, ckpt=64, 
     cb = codec.compress(src)
     out, st = codec.decompress(cb)  # sidecar segment decoder
     out2, st2 = codec.decompress(cb, use_sidecar=False)  # serial, reference order
+    out3, side3, st3 = codec.build_sidecar(cb)  # serial, recording the checkpoints
     torch.cuda.synchronize()
     assert int(cb["status"].abs().max()) == 0, cb["status"].cpu().numpy()[:8]
     assert int(st.abs().max()) == 0, st.cpu().numpy()[:8]
     assert int(st2.abs().max()) == 0, st2.cpu().numpy()[:8]
+    assert int(st3.abs().max()) == 0, st3.cpu().numpy()[:8]
     assert torch.equal(out, src)
     assert torch.equal(out2, src)
+    assert torch.equal(out3, src)
     nb = codec.n_blocks(n_total)
+    spb = codec.side_per_block
+    assert torch.equal(side3[: nb * spb], cb["sidecar"][: nb * spb]), "rebuilt sidecar != encoder sidecar"
     host = src.cpu().numpy()
     blocks = range(nb) if check_all else sorted({0, nb // 2, nb - 1})
     for b in blocks:

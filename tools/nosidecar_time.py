@@ -19,7 +19,8 @@ only = os.environ.get("NS_CASES")
 for name, kind, prob, tl in cases:
     if only and name not in only.split(","):
         continue
-    codec = BlockCodec(ckpt_interval=128, table_log=tl)
+    ns = int(os.environ.get("NS_STATES", 2))
+    codec = BlockCodec(ckpt_interval=128, table_log=tl, nstates=ns)
     src = codec.generate(kind, prob, 0x5EED0002, n)
     cb = codec.compress(src)
     out = torch.empty(n, dtype=torch.uint8, device="cuda")
@@ -39,6 +40,6 @@ for name, kind, prob, tl in cases:
     torch.cuda.synchronize()
     side_ok = bool(torch.equal(o2, src)) and int(st2.abs().max()) == 0 and bool(torch.equal(side2, cb["sidecar"]))
     ratio = int(cb["comp_len"].sum()) / n
-    print(f"{name}: ratio {ratio:.3f}  sidecar {res[True][0] * 1e3:.2f} ms ({n / res[True][0] / 2**30:.0f} GiB/s, "
+    print(f"{name} ({ns}-state): ratio {ratio:.3f}  sidecar {res[True][0] * 1e3:.2f} ms ({n / res[True][0] / 2**30:.0f} GiB/s, "
           f"ok={res[True][1]})  no sidecar {res[False][0] * 1e3:.2f} ms ({n / res[False][0] / 2**30:.1f} GiB/s, "
           f"ok={res[False][1]})  build_sidecar ok={side_ok}", flush=True)
