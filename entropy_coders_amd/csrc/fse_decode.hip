@@ -477,6 +477,7 @@ __global__ __launch_bounds__(64) void dtable_blocks_kernel(DtParams P) {
     // (the decoder's visit reads norm only); 7 KB per workgroup at L = 11
     __shared__ __attribute__((aligned(16))) uint16_t rk[SIZE];
     static_assert(SIZE + 256 * 4 + 256 * 2 <= SIZE * 2, "rank table must cover occ, cnt and cumul");
+    __shared__ uint64_t pm[64];  // rank peer masks (lds_peers)
     uint8_t* occ = reinterpret_cast<uint8_t*>(rk);
     uint32_t* cnt = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(rk) + SIZE);
     uint16_t* cumul = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(rk) + SIZE + 1024);
@@ -520,7 +521,7 @@ __global__ __launch_bounds__(64) void dtable_blocks_kernel(DtParams P) {
             dt[i] = Dte<LMAX>::make(nb, s, (nx << nb) - size);
         };
         // two-pass ranks need 2^L / 64 per-chunk registers: up to L = 12
-        if (LMAX <= 12) rc = wave_build_spread<SIZE / 64u>(norm, L, tl, sym_at, occ, cumul, cnt, visit, rk);
+        if (LMAX <= 12) rc = wave_build_spread<SIZE / 64u>(norm, L, tl, sym_at, occ, cumul, cnt, visit, rk, pm);
         else rc = wave_build_spread(norm, L, tl, sym_at, occ, cumul, cnt, visit);
     }
     if (lane == 0) P.dtinfo[gb] = rc == FSE_OK ? (int32_t)((uint32_t)hl | (L << 16)) : rc;

@@ -89,6 +89,17 @@ __device__ __forceinline__ uint64_t match_key(uint32_t key, uint64_t active, uin
 }
 __device__ __forceinline__ uint32_t key_bits(uint32_t tl) { return tl <= 1u ? 1u : 32u - (uint32_t)__clz(tl - 1u); }
 
+// The same peer mask for keys < 64 through LDS: every lane clears slot
+// `lane` of the 64 u64 masks `pm`, ORs its lane bit into pm[key] and reads
+// pm[key] back.  Three LDS instructions instead of ~9 VALU per key bit; one
+// wave's LDS instructions complete in order, so each step sees the whole
+// previous one (the compiler keeps their order: the slots may alias).
+__device__ __forceinline__ uint64_t lds_peers(uint32_t key, uint64_t* pm, uint64_t lanebit) {
+    pm[lane_id()] = 0;
+    __hip_atomic_fetch_or(&pm[key], lanebit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    return __hip_atomic_load(&pm[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
 // ---------------------------------------------------------------------------
 // Histogram::new (histogram.rs:18-66): 256-bin count of one block by one
 // wave.  HSUB = 8 LDS sub-histograms (lane % 8), interleaved bin-major
@@ -747,7 +758,7 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t v) { return dpp0<0x138, 0
 template <uint32_t MAXCH = 64, typename Visit>  // MAXCH: 2^LMAX / 64 chunks (two-pass ranks)
 __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_t tl, uint8_t* sym_at,
                                         uint8_t* occ_sym, uint16_t* cumul, uint32_t* cnt, Visit visit,
-                                        uint16_t* RK = nullptr) {
+                                        uint16_t* RK = nullptr, uint64_t* PM = nullptr) {
     const uint32_t lane = lane_id();
     const uint32_t size = 1u << L;
     const uint32_t mask = size - 1u;
@@ -840,6 +851,7 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
         // (written by its lowest lane) and each lane's peers below, packed
         // four chunks per register
         const uint32_t nch = size / WAVE, kb = key_bits(tl);
+        const uint64_t lanebit = 1ull << lane;
         for (uint32_t i = lane; i < nch * 64u / 8u; i += WAVE) reinterpret_cast<uint4*>(RK)[i] = make_uint4(0, 0, 0, 0);
         wave_sync();
         uint32_t below[(MAXCH + 3) / 4];
@@ -848,7 +860,7 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
             if ((t & 3u) == 0) below[t >> 2] = 0;
             if (t < nch) {
                 const uint32_t sy = sym_at[t * WAVE + lane];
-                const uint64_t peers = match_key(sy, ~0ull, kb);
+                const uint64_t peers = PM ? lds_peers(sy, PM, lanebit) : match_key(sy, ~0ull, kb);
                 const uint32_t bl = (uint32_t)__popcll(peers & lanemask_lt());
                 if (bl == 0) RK[t * 64u + sy] = (uint16_t)__popcll(peers);
                 below[t >> 2] |= bl << (8u * (t & 3u));
@@ -880,13 +892,16 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
         wave_sync();
         return FSE_OK;
     }
-    // occurrence ranks in ascending position order
+    // occurrence ranks in ascending position order (PM: occ_sym is dead by
+    // now, so the caller may alias the masks into it)
+    const bool lds_match = PM != nullptr && tl <= 64u && size >= WAVE;
+    const uint64_t lanebit = 1ull << lane;
     for (uint32_t base = 0; base < size; base += WAVE) {
         uint32_t i = base + lane;
         bool act = i < size;
         uint64_t active = __ballot(act);
         uint32_t s = act ? sym_at[i] : 0u;
-        uint64_t peers = match_key(s, active, key_bits(tl));
+        uint64_t peers = lds_match ? lds_peers(s, PM, lanebit) : match_key(s, active, key_bits(tl));
         uint32_t before = act ? cnt[s] : 0u;
         uint32_t r = before + (uint32_t)__popcll(peers & lanemask_lt());
         wave_sync();
@@ -895,166 +910,6 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
         if (act) visit(i, s, r);
         wave_sync();
     }
-    return FSE_OK;
-}
-
-// ---------------------------------------------------------------------------
-// Workgroup version of wave_build_spread for NW waves (decoder tables,
-// fse.rs:280-338): the occurrence max-fill, the spread walk and the rank
-// walk are each split into NW contiguous ranges with cross-wave carries
-// through LDS.  Ranks use per-wave counters, then an exclusive prefix of
-// the counters over waves.  visit(i, s, r) runs after every read of
-// sym_at/occ_sym, so the caller may alias those into its output table.
-// All waves of the workgroup must call it.
-// ---------------------------------------------------------------------------
-template <int NW, int LMAX, typename Visit>
-__device__ inline int block_build_spread(const int32_t* norm, uint32_t L, uint32_t tl, uint8_t* sym_at,
-                                         uint8_t* occ_sym, uint16_t* cumul, uint32_t* cnt /*[NW][256]*/,
-                                         uint32_t* wscr /*[NW + 4]*/, Visit visit) {
-    constexpr uint32_t RMAX = ((1u << LMAX) + 64u * NW - 1u) / (64u * NW);
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-    const uint32_t size = 1u << L;
-    const uint32_t mask = size - 1u;
-    for (uint32_t i = tid; i < size; i += 64u * NW) { occ_sym[i] = 0; sym_at[i] = 0; }
-    for (uint32_t i = tid; i < 256u * NW; i += 64u * NW) cnt[i] = 0;
-    __syncthreads();
-    if (wv == 0) {  // per-symbol scans (fse.rs:119-129)
-        uint32_t cp[4], pos_n[4], neg[4];
-        uint32_t sum_c = 0, sum_p = 0, sum_neg = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t s = lane * 4u + k;
-            const int32_t v = (s < tl) ? norm[s] : 0;
-            neg[k] = (v == -1 || v < -1) ? 1u : 0u;
-            pos_n[k] = v > 0 ? (uint32_t)v : 0u;
-            cp[k] = (v == -1) ? 1u : pos_n[k];
-            sum_c += cp[k];
-            sum_p += pos_n[k];
-            sum_neg += neg[k];
-        }
-        const uint32_t ex_c = wave_incl_sum(sum_c) - sum_c;
-        const uint32_t ex_p = wave_incl_sum(sum_p) - sum_p;
-        const uint32_t ex_n = wave_incl_sum(sum_neg) - sum_neg;
-        const uint32_t total_neg = bcast63(ex_n + sum_neg);
-        const uint32_t total_pos = bcast63(ex_p + sum_p);
-        const bool ok = total_pos + total_neg <= size;
-        uint32_t c = ex_c, p = ex_p, ng = ex_n;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t s = lane * 4u + k;
-            cumul[s] = (uint16_t)c;
-            if (ok && pos_n[k]) occ_sym[p] = (uint8_t)s;
-            if (ok && neg[k]) sym_at[size - 1u - ng] = (uint8_t)s;
-            c += cp[k];
-            p += pos_n[k];
-            ng += neg[k];
-        }
-        if (lane == 0) {
-            wscr[NW] = total_pos;
-            wscr[NW + 1] = total_neg;
-            wscr[NW + 2] = ok ? 0u : 1u;
-        }
-    }
-    __syncthreads();
-    const uint32_t total_pos = wscr[NW], total_neg = wscr[NW + 1];
-    if (wscr[NW + 2]) return FSE_ERR_BAD_TABLE;
-    const int32_t ht = (int32_t)size - 1 - (int32_t)total_neg;
-    // occurrence owners: forward max-fill, per-wave ranges + carry
-    const uint32_t orange = ((total_pos + NW - 1u) / NW + 63u) & ~63u;
-    const uint32_t o0 = wv * orange, o1 = min(o0 + orange, total_pos);
-    {
-        uint32_t carry = 0;
-        for (uint32_t base = o0; base < o1; base += WAVE) {
-            const uint32_t j = base + lane;
-            const uint32_t v = (j < o1) ? occ_sym[j] : 0u;
-            const uint32_t f = max(wave_incl_max(v), carry);
-            if (j < o1) occ_sym[j] = (uint8_t)f;
-            carry = bcast63(f);
-        }
-        if (lane == 0) wscr[wv] = carry;
-    }
-    __syncthreads();
-    {
-        uint32_t cin = 0;
-        for (uint32_t w = 0; w < wv; ++w) cin = max(cin, wscr[w]);
-        if (cin)
-            for (uint32_t j = o0 + lane; j < o1; j += WAVE) occ_sym[j] = (uint8_t)max((uint32_t)occ_sym[j], cin);
-    }
-    __syncthreads();
-    // spread (fse.rs:139-151): j-th valid multiplier -> position
-    const uint32_t step = (size >> 3) * 5u + 3u;
-    const uint32_t mrange = (size + NW - 1u) / NW;
-    const uint32_t m0 = wv * mrange, m1 = min(m0 + mrange, size);
-    {
-        uint32_t cntv = 0;
-        for (uint32_t base = m0; base < m1; base += WAVE) {
-            const uint32_t m = base + lane;
-            const bool valid = m < m1 && (int32_t)((m * step) & mask) <= ht;
-            cntv += (uint32_t)__popcll(__ballot(valid));
-        }
-        if (lane == 0) wscr[wv] = cntv;
-    }
-    __syncthreads();
-    {
-        uint32_t j0 = 0, tot = 0;
-        for (uint32_t w = 0; w < NW; ++w) {
-            if (w < wv) j0 += wscr[w];
-            tot += wscr[w];
-        }
-        if (tot != total_pos) return FSE_ERR_BAD_TABLE;  // position != 0 assert
-        for (uint32_t base = m0; base < m1; base += WAVE) {
-            const uint32_t m = base + lane;
-            const uint32_t p = (m * step) & mask;
-            const bool valid = m < m1 && (int32_t)p <= ht;
-            const uint64_t bal = __ballot(valid);
-            const uint32_t j = j0 + (uint32_t)__popcll(bal & lanemask_lt());
-            if (valid) sym_at[p] = occ_sym[j];
-            j0 += (uint32_t)__popcll(bal);
-        }
-    }
-    __syncthreads();
-    // ranks: local ranks per wave range, then per-symbol prefix over waves
-    const uint32_t prange = (size + NW - 1u) / NW;
-    const uint32_t i0 = wv * prange, i1 = min(i0 + prange, size);
-    uint32_t* mycnt = cnt + wv * 256u;
-    uint32_t rs[RMAX];  // local rank << 8 | symbol, per round
-#pragma unroll
-    for (uint32_t r = 0; r < RMAX; ++r) {
-        const uint32_t base = i0 + r * WAVE;
-        rs[r] = 0;
-        if (base < i1) {
-            const uint32_t i = base + lane;
-            const bool act = i < i1;
-            const uint64_t active = __ballot(act);
-            const uint32_t s = act ? sym_at[i] : 0u;
-            const uint64_t peers = match_key(s, active, key_bits(tl));
-            const uint32_t before = act ? mycnt[s] : 0u;
-            const uint32_t rk = before + (uint32_t)__popcll(peers & lanemask_lt());
-            wave_sync();
-            if (act && (peers & lanemask_lt()) == 0) mycnt[s] = before + (uint32_t)__popcll(peers);
-            wave_sync();
-            rs[r] = (rk << 8) | s;
-        }
-    }
-    __syncthreads();
-    for (uint32_t s = tid; s < 256u; s += 64u * NW) {
-        uint32_t run = 0;
-        for (uint32_t w = 0; w < NW; ++w) {
-            const uint32_t c = cnt[w * 256u + s];
-            cnt[w * 256u + s] = run;
-            run += c;
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t r = 0; r < RMAX; ++r) {
-        const uint32_t i = i0 + r * WAVE + lane;
-        if (i0 + r * WAVE < i1 && i < i1) {
-            const uint32_t s = rs[r] & 0xFFu;
-            visit(i, s, (rs[r] >> 8) + mycnt[s]);
-        }
-    }
-    __syncthreads();
     return FSE_OK;
 }
 

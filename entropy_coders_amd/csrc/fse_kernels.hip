@@ -482,7 +482,8 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
             rc = wave_build_spread(sm.ph.p1.norm, L, tl, sm.ph.p1.u.sp.sym_at, sm.ph.p1.u.sp.occ_sym, sm.ph.p1.cumul, sm.ph.p1.cnt,
                                    [&](uint32_t i, uint32_t s, uint32_t r) {
                                        st[cumul[s] + r] = (uint16_t)(size + i);  // fse.rs:157-162
-                                   });
+                                   },
+                                   nullptr, reinterpret_cast<uint64_t*>(sm.ph.p1.u.sp.occ_sym));
             // symbol transforms, fse.rs:165-188 (total == cumul[s]), with
             // the stateTable's LDS address folded into deltaFindState
             const uint32_t stb = lds_addr_of(&sm.st[b][0]);
