@@ -26,8 +26,8 @@ EXPORTS = (
     "fsehip_copy_blocks",
     "histogram_new", "histogram_normalize", "histogram_normalize_optimal", "norm_histogram_new",
     "norm_histogram_write", "norm_histogram_read", "encode_table_new", "decode_table_new", "fse_compress_nh",
-    "bitstack_write", "bitstack_read", "bitstream_read",
-    "fsehip_bitstack_write", "fsehip_bitstack_read", "fsehip_bitstream_read",
+    "bitstack_write", "bitstack_read", "bitstream_read", "bitstream_read_ops",
+    "fsehip_bitstack_write", "fsehip_bitstack_read", "fsehip_bitstream_read", "fsehip_bitstream_read_ops",
 )
 
 STATUS = {
@@ -131,9 +131,11 @@ def load() -> C.CDLL:
     lib.bitstack_write.argtypes = [P, P, sz, P, sz, C.POINTER(sz), C.POINTER(u64)]
     lib.bitstack_read.argtypes = [P, sz, P, sz, P, C.POINTER(sz), C.POINTER(C.c_int)]
     lib.bitstream_read.argtypes = [P, sz, u64, P, sz, P, C.POINTER(sz), C.POINTER(u64)]
+    lib.bitstream_read_ops.argtypes = [P, sz, u64, P, P, sz, P, C.POINTER(sz), C.POINTER(u64)]
     lib.fsehip_bitstack_write.argtypes = [P, P, u64, P, u64, P, P]
     lib.fsehip_bitstack_read.argtypes = [P, u64, P, u64, P, P, P]
     lib.fsehip_bitstream_read.argtypes = [P, u64, u64, P, u64, P, P, P]
+    lib.fsehip_bitstream_read_ops.argtypes = [P, u64, u64, P, P, u64, P, P, P]
     lib.fsehip_device_count.argtypes = []
     lib.fsehip_version.restype = C.c_char_p
     for name in EXPORTS:

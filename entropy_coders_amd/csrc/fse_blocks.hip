@@ -205,15 +205,21 @@ __global__ __launch_bounds__(64) void table_kernel(const fse_norm_histogram* nh,
 //   bits_unpack     BitStackReader (stack_reader.rs:17-215: field i ends at
 //                   top - S_i, read downwards from the marker) or
 //                   BitStreamReader (stream_reader.rs:16-135: field i starts
-//                   at S_i); reads past the available bits fail, and
-//                   result[0] = the index of the first failing read
+//                   at S_i, and may be a read, a peek or an advance_by);
+//                   steps past the available bits fail, and result[0] = the
+//                   index of the first failing step
 // ------------------------------------------------------------------------
 constexpr uint32_t BT_THREADS = 256, BT_PER = 16, BT_TILE = BT_THREADS * BT_PER;
 
-__device__ __forceinline__ uint32_t thread_bits(const uint8_t* nbits, uint64_t count, uint64_t i0) {
+// Bits field i moves the position: its width, or 0 for a peek (ops[i] ==
+// FSE_BITS_PEEK; `ops` may be null: all reads / writes).
+__device__ __forceinline__ uint32_t field_advance(const uint8_t* nbits, const uint8_t* ops, uint64_t i) {
+    return ops && ops[i] == FSE_BITS_PEEK ? 0u : min((uint32_t)nbits[i], 32u);
+}
+__device__ __forceinline__ uint32_t thread_bits(const uint8_t* nbits, const uint8_t* ops, uint64_t count, uint64_t i0) {
     uint32_t s = 0;
 #pragma unroll
-    for (uint32_t k = 0; k < BT_PER; ++k) s += i0 + k < count ? min((uint32_t)nbits[i0 + k], 32u) : 0u;
+    for (uint32_t k = 0; k < BT_PER; ++k) s += i0 + k < count ? field_advance(nbits, ops, i0 + k) : 0u;
     return s;
 }
 
@@ -235,12 +241,12 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh, ui
     return base + incl - v;
 }
 
-__global__ __launch_bounds__(256) void bits_tile_sum(const uint8_t* __restrict__ nbits, uint64_t count,
-                                                     uint32_t* __restrict__ tile_sum) {
+__global__ __launch_bounds__(256) void bits_tile_sum(const uint8_t* __restrict__ nbits, const uint8_t* __restrict__ ops,
+                                                     uint64_t count, uint32_t* __restrict__ tile_sum) {
     __shared__ uint32_t sh[BT_THREADS / 64u];
     const uint64_t i0 = (uint64_t)blockIdx.x * BT_TILE + (uint64_t)threadIdx.x * BT_PER;
     uint32_t tot;
-    (void)block_excl_scan(thread_bits(nbits, count, i0), sh, &tot);
+    (void)block_excl_scan(thread_bits(nbits, ops, count, i0), sh, &tot);
     if (threadIdx.x == 0) tile_sum[blockIdx.x] = tot;
 }
 
@@ -290,7 +296,7 @@ __global__ __launch_bounds__(256) void bits_pack(const uint32_t* __restrict__ va
     __shared__ uint32_t sh[BT_THREADS / 64u];
     const uint64_t i0 = (uint64_t)blockIdx.x * BT_TILE + (uint64_t)threadIdx.x * BT_PER;
     uint32_t tot;
-    const uint64_t start = tile_off[blockIdx.x] + block_excl_scan(thread_bits(nbits, count, i0), sh, &tot);
+    const uint64_t start = tile_off[blockIdx.x] + block_excl_scan(thread_bits(nbits, nullptr, count, i0), sh, &tot);
     if ((*total + 31u) >> 5 > lim_words) return;  // the host checked the capacity; never write past it
     // the thread's fields as one bit run from `start`: a 64-bit accumulator,
     // each completed word stored as it completes; the first word (shared
@@ -330,12 +336,13 @@ __device__ __forceinline__ int64_t bits_avail(const uint8_t* in, uint64_t n_byte
 
 __global__ __launch_bounds__(256) void bits_unpack(const uint8_t* __restrict__ in, uint64_t n_bytes,
                                                    uint64_t total_bits, int stack, const uint8_t* __restrict__ nbits,
-                                                   uint64_t count, const uint64_t* __restrict__ tile_off,
+                                                   const uint8_t* __restrict__ ops, uint64_t count,
+                                                   const uint64_t* __restrict__ tile_off,
                                                    uint32_t* __restrict__ vals, uint64_t* __restrict__ result) {
     __shared__ uint32_t sh[BT_THREADS / 64u];
     const uint64_t i0 = (uint64_t)blockIdx.x * BT_TILE + (uint64_t)threadIdx.x * BT_PER;
     uint32_t tot;
-    uint64_t s = tile_off[blockIdx.x] + block_excl_scan(thread_bits(nbits, count, i0), sh, &tot);
+    uint64_t s = tile_off[blockIdx.x] + block_excl_scan(thread_bits(nbits, ops, count, i0), sh, &tot);
     const int64_t av = bits_avail(in, n_bytes, total_bits, stack);
     const uint64_t avail = av < 0 ? 0u : (uint64_t)av;
     const uint32_t* w = reinterpret_cast<const uint32_t*>(in);
@@ -343,10 +350,13 @@ __global__ __launch_bounds__(256) void bits_unpack(const uint8_t* __restrict__ i
         const uint64_t i = i0 + k;
         if (i >= count) break;
         const uint32_t nb = min((uint32_t)nbits[i], 32u);
+        const uint32_t op = ops ? ops[i] : FSE_BITS_READ;
         uint32_t v = 0;
-        if (av < 0 || s + nb > avail) {  // peek fails: None / Err(UnexpectedEof)
+        // read, peek and advance_by all fail past the available bits
+        // (stream_reader.rs:70-72, 85-87); advance_by returns no value
+        if (av < 0 || s + nb > avail) {  // None / Err(UnexpectedEof)
             atomicMin(reinterpret_cast<unsigned long long*>(result), (unsigned long long)i);
-        } else if (nb) {
+        } else if (nb && op != FSE_BITS_ADVANCE) {
             const uint64_t lo = stack ? avail - s - nb : s;  // first bit of the field
             const uint64_t wi = lo >> 5;
             const uint32_t sh5 = (uint32_t)(lo & 31u);
@@ -354,7 +364,7 @@ __global__ __launch_bounds__(256) void bits_unpack(const uint8_t* __restrict__ i
             v = (uint32_t)(x >> sh5) & (nb == 32u ? 0xFFFFFFFFu : (1u << nb) - 1u);
         }
         vals[i] = v;
-        s += nb;
+        s += op == FSE_BITS_PEEK ? 0u : nb;
     }
 }
 
@@ -393,10 +403,10 @@ hipError_t launch_table(const fse_norm_histogram* nh, int enc, fse_encode_table*
 
 uint64_t bits_tiles(uint64_t count) { return (count + BT_TILE - 1u) / BT_TILE; }
 
-hipError_t launch_bits_scan(const uint8_t* nbits, uint64_t count, uint32_t* tile_sum, uint64_t* tile_off,
-                            uint64_t* total, hipStream_t s) {
+hipError_t launch_bits_scan(const uint8_t* nbits, const uint8_t* ops, uint64_t count, uint32_t* tile_sum,
+                            uint64_t* tile_off, uint64_t* total, hipStream_t s) {
     const uint64_t nt = bits_tiles(count);
-    if (nt) hipLaunchKernelGGL(bits_tile_sum, dim3((uint32_t)nt), dim3(BT_THREADS), 0, s, nbits, count, tile_sum);
+    if (nt) hipLaunchKernelGGL(bits_tile_sum, dim3((uint32_t)nt), dim3(BT_THREADS), 0, s, nbits, ops, count, tile_sum);
     hipLaunchKernelGGL(bits_tile_scan, dim3(1), dim3(1024), 0, s, tile_sum, nt, tile_off, total);
     return hipGetLastError();
 }
@@ -414,13 +424,13 @@ hipError_t launch_bits_pack(const uint32_t* vals, const uint8_t* nbits, uint64_t
 }
 
 hipError_t launch_bits_unpack(const uint8_t* in, uint64_t n_bytes, uint64_t total_bits, int stack,
-                              const uint8_t* nbits, uint64_t count, const uint64_t* tile_off, const uint64_t* total,
-                              uint32_t* vals, uint64_t* result, hipStream_t s) {
+                              const uint8_t* nbits, const uint8_t* ops, uint64_t count, const uint64_t* tile_off,
+                              const uint64_t* total, uint32_t* vals, uint64_t* result, hipStream_t s) {
     hipLaunchKernelGGL(bits_read_init, dim3(1), dim3(1), 0, s, in, n_bytes, total_bits, stack, count, total, result);
     const uint64_t nt = bits_tiles(count);
     if (nt)
         hipLaunchKernelGGL(bits_unpack, dim3((uint32_t)nt), dim3(BT_THREADS), 0, s, in, n_bytes, total_bits, stack,
-                           nbits, count, tile_off, vals, result);
+                           nbits, ops, count, tile_off, vals, result);
     return hipGetLastError();
 }
 

@@ -748,15 +748,16 @@ int fse_compress_nh(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, 
 
 // Scan of the widths into the workspace of `stream`; returns the device
 // tile offsets and total (valid in stream order).
-static int bits_scan(Lease& lease, const uint8_t* d_nbits, uint64_t count, uint64_t** tile_off, uint64_t** total,
-                     fsehip_stream_t stream) {
+static int bits_scan(Lease& lease, const uint8_t* d_nbits, const uint8_t* d_ops, uint64_t count, uint64_t** tile_off,
+                     uint64_t** total, fsehip_stream_t stream) {
     const uint64_t nt = fsehip::bits_tiles(count);
     uint8_t* w = static_cast<uint8_t*>(lease.get(SCRATCH_BITS, 16 + nt * 12 + 16));
     if (!w) return FSE_ERR_HIP;
     *total = reinterpret_cast<uint64_t*>(w);
     *tile_off = reinterpret_cast<uint64_t*>(w + 16);
     uint32_t* tile_sum = reinterpret_cast<uint32_t*>(w + 16 + nt * 8);
-    return fsehip::launch_bits_scan(d_nbits, count, tile_sum, *tile_off, *total, static_cast<hipStream_t>(stream)) ==
+    return fsehip::launch_bits_scan(d_nbits, d_ops, count, tile_sum, *tile_off, *total,
+                                    static_cast<hipStream_t>(stream)) ==
                    hipSuccess
                ? FSE_OK
                : FSE_ERR_HIP;
@@ -769,7 +770,7 @@ int fsehip_bitstack_write(const uint32_t* d_vals, const uint8_t* d_nbits, uint64
     if (!device_ok()) return FSE_ERR_NO_DEVICE;
     Lease lease(stream);
     uint64_t *tile_off = nullptr, *total = nullptr;
-    int rc = bits_scan(lease, d_nbits, count, &tile_off, &total, stream);
+    int rc = bits_scan(lease, d_nbits, nullptr, count, &tile_off, &total, stream);
     if (rc) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (fsehip::launch_bits_pack(d_vals, d_nbits, count, tile_off, total, reinterpret_cast<uint32_t*>(d_out),
@@ -779,14 +780,15 @@ int fsehip_bitstack_write(const uint32_t* d_vals, const uint8_t* d_nbits, uint64
 }
 
 static int bits_read_dev(const uint8_t* d_in, uint64_t n_bytes, uint64_t total_bits, int stack, const uint8_t* d_nbits,
-                         uint64_t count, uint32_t* d_vals, uint64_t* d_result, fsehip_stream_t stream) {
+                         const uint8_t* d_ops, uint64_t count, uint32_t* d_vals, uint64_t* d_result,
+                         fsehip_stream_t stream) {
     if ((count && (!d_nbits || !d_vals)) || !d_result || (!d_in && n_bytes)) return FSE_ERR_BAD_ARG;
     if (!device_ok()) return FSE_ERR_NO_DEVICE;
     Lease lease(stream);
     uint64_t *tile_off = nullptr, *total = nullptr;
-    int rc = bits_scan(lease, d_nbits, count, &tile_off, &total, stream);
+    int rc = bits_scan(lease, d_nbits, d_ops, count, &tile_off, &total, stream);
     if (rc) return rc;
-    return fsehip::launch_bits_unpack(d_in, n_bytes, total_bits, stack, d_nbits, count, tile_off, total, d_vals,
+    return fsehip::launch_bits_unpack(d_in, n_bytes, total_bits, stack, d_nbits, d_ops, count, tile_off, total, d_vals,
                                       d_result, static_cast<hipStream_t>(stream)) == hipSuccess
                ? FSE_OK
                : FSE_ERR_HIP;
@@ -794,13 +796,19 @@ static int bits_read_dev(const uint8_t* d_in, uint64_t n_bytes, uint64_t total_b
 
 int fsehip_bitstack_read(const uint8_t* d_in, uint64_t n_bytes, const uint8_t* d_nbits, uint64_t count,
                          uint32_t* d_vals, uint64_t* d_result, fsehip_stream_t stream) {
-    return bits_read_dev(d_in, n_bytes, 0, 1, d_nbits, count, d_vals, d_result, stream);
+    return bits_read_dev(d_in, n_bytes, 0, 1, d_nbits, nullptr, count, d_vals, d_result, stream);
+}
+
+int fsehip_bitstream_read_ops(const uint8_t* d_in, uint64_t n_bytes, uint64_t total_bits, const uint8_t* d_nbits,
+                              const uint8_t* d_ops, uint64_t count, uint32_t* d_vals, uint64_t* d_result,
+                              fsehip_stream_t stream) {
+    if (n_bytes == 0 || (total_bits + 7u) / 8u != n_bytes) return FSE_ERR_BAD_ARG;  // stream_reader.rs:17-21 asserts
+    return bits_read_dev(d_in, n_bytes, total_bits, 0, d_nbits, d_ops, count, d_vals, d_result, stream);
 }
 
 int fsehip_bitstream_read(const uint8_t* d_in, uint64_t n_bytes, uint64_t total_bits, const uint8_t* d_nbits,
                           uint64_t count, uint32_t* d_vals, uint64_t* d_result, fsehip_stream_t stream) {
-    if (n_bytes == 0 || (total_bits + 7u) / 8u != n_bytes) return FSE_ERR_BAD_ARG;  // stream_reader.rs:17-21 asserts
-    return bits_read_dev(d_in, n_bytes, total_bits, 0, d_nbits, count, d_vals, d_result, stream);
+    return fsehip_bitstream_read_ops(d_in, n_bytes, total_bits, d_nbits, nullptr, count, d_vals, d_result, stream);
 }
 
 int bitstack_write(const uint32_t* vals, const uint8_t* nbits, size_t count, uint8_t* dst, size_t dst_cap,
@@ -831,21 +839,23 @@ int bitstack_write(const uint32_t* vals, const uint8_t* nbits, size_t count, uin
 }
 
 static int bits_read_host(const uint8_t* src, size_t n, uint64_t total_bits, int stack, const uint8_t* nbits,
-                          size_t count, uint32_t* vals, uint64_t res[3]) {
+                          const uint8_t* ops, size_t count, uint32_t* vals, uint64_t res[3]) {
     if ((count && (!nbits || !vals)) || (!src && n)) return FSE_ERR_BAD_ARG;
     if (!device_ok()) return FSE_ERR_NO_DEVICE;
     uint8_t* d_in = g_stage.get(0, round_up(n, 4) + 16);
     uint8_t* d_nb = g_stage.get(1, count + 16);
     uint8_t* d_v = g_stage.get(5, count * 4 + 16);
     uint8_t* d_res = g_stage.get(2, 32);
-    if (!d_in || !d_nb || !d_v || !d_res) return FSE_ERR_HIP;
+    uint8_t* d_ops = ops ? g_stage.get(3, count + 16) : nullptr;
+    if (!d_in || !d_nb || !d_v || !d_res || (ops && !d_ops)) return FSE_ERR_HIP;
     if (hipMemset(d_in, 0, round_up(n, 4) + 16) != hipSuccess) return FSE_ERR_HIP;
     if (n && hipMemcpy(d_in, src, n, hipMemcpyHostToDevice) != hipSuccess) return FSE_ERR_HIP;
     if (count && hipMemcpy(d_nb, nbits, count, hipMemcpyHostToDevice) != hipSuccess) return FSE_ERR_HIP;
+    if (ops && count && hipMemcpy(d_ops, ops, count, hipMemcpyHostToDevice) != hipSuccess) return FSE_ERR_HIP;
     uint64_t* r = reinterpret_cast<uint64_t*>(d_res);
     int rc = stack ? fsehip_bitstack_read(d_in, n, d_nb, count, reinterpret_cast<uint32_t*>(d_v), r, nullptr)
-                   : fsehip_bitstream_read(d_in, n, total_bits, d_nb, count, reinterpret_cast<uint32_t*>(d_v), r,
-                                           nullptr);
+                   : fsehip_bitstream_read_ops(d_in, n, total_bits, d_nb, d_ops, count,
+                                               reinterpret_cast<uint32_t*>(d_v), r, nullptr);
     if (rc) return rc;
     if (hipMemcpy(res, r, 24, hipMemcpyDeviceToHost) != hipSuccess) return FSE_ERR_HIP;
     if ((int64_t)res[2] != FSE_OK) return (int)(int64_t)res[2];
@@ -856,7 +866,7 @@ static int bits_read_host(const uint8_t* src, size_t n, uint64_t total_bits, int
 int bitstack_read(const uint8_t* src, size_t n, const uint8_t* nbits, size_t count, uint32_t* vals, size_t* n_read,
                   int* finished) {
     uint64_t res[3] = {0, 0, 0};
-    int rc = bits_read_host(src, n, 0, 1, nbits, count, vals, res);
+    int rc = bits_read_host(src, n, 0, 1, nbits, nullptr, count, vals, res);
     if (rc) return rc;
     if (n_read) *n_read = (size_t)res[0];
     // finish() after the successful reads: all bits consumed (reads stop at
@@ -865,18 +875,27 @@ int bitstack_read(const uint8_t* src, size_t n, const uint8_t* nbits, size_t cou
     return FSE_OK;
 }
 
-int bitstream_read(const uint8_t* src, size_t n, uint64_t total_bits, const uint8_t* nbits, size_t count,
-                   uint32_t* vals, size_t* n_read, uint64_t* bits_left) {
+int bitstream_read_ops(const uint8_t* src, size_t n, uint64_t total_bits, const uint8_t* nbits, const uint8_t* ops,
+                       size_t count, uint32_t* vals, size_t* n_done, uint64_t* bits_left) {
+    if (ops)
+        for (size_t i = 0; i < count; ++i)
+            if (ops[i] > FSE_BITS_ADVANCE) return FSE_ERR_BAD_ARG;
     uint64_t res[3] = {0, 0, 0};
-    int rc = bits_read_host(src, n, total_bits, 0, nbits, count, vals, res);
+    int rc = bits_read_host(src, n, total_bits, 0, nbits, ops, count, vals, res);
     if (rc) return rc;
-    if (n_read) *n_read = (size_t)res[0];
+    if (n_done) *n_done = (size_t)res[0];
     if (bits_left) {
         uint64_t used = 0;
-        for (size_t i = 0; i < res[0]; ++i) used += std::min<uint32_t>(nbits[i], 32u);
+        for (size_t i = 0; i < res[0]; ++i)
+            if (!ops || ops[i] != FSE_BITS_PEEK) used += std::min<uint32_t>(nbits[i], 32u);
         *bits_left = total_bits - used;
     }
     return FSE_OK;
+}
+
+int bitstream_read(const uint8_t* src, size_t n, uint64_t total_bits, const uint8_t* nbits, size_t count,
+                   uint32_t* vals, size_t* n_read, uint64_t* bits_left) {
+    return bitstream_read_ops(src, n, total_bits, nbits, nullptr, count, vals, n_read, bits_left);
 }
 
 // Diagnostics only (not part of include/fsehip.h): resident workgroups per CU.

@@ -93,13 +93,13 @@ hipError_t launch_table(const fse_norm_histogram* nh, int enc, fse_encode_table*
 // Bitstream primitives: a tile scan of the field widths (tile_sum: u32 per
 // tile, tile_off: u64 per tile, total: u64), then pack or unpack.
 uint64_t bits_tiles(uint64_t count);
-hipError_t launch_bits_scan(const uint8_t* nbits, uint64_t count, uint32_t* tile_sum, uint64_t* tile_off,
-                            uint64_t* total, hipStream_t s);
+hipError_t launch_bits_scan(const uint8_t* nbits, const uint8_t* ops, uint64_t count, uint32_t* tile_sum,
+                            uint64_t* tile_off, uint64_t* total, hipStream_t s);
 hipError_t launch_bits_pack(const uint32_t* vals, const uint8_t* nbits, uint64_t count, const uint64_t* tile_off,
                             const uint64_t* total, uint32_t* out, uint64_t lim_words, hipStream_t s);
 hipError_t launch_bits_unpack(const uint8_t* in, uint64_t n_bytes, uint64_t total_bits, int stack,
-                              const uint8_t* nbits, uint64_t count, const uint64_t* tile_off, const uint64_t* total,
-                              uint32_t* vals, uint64_t* result, hipStream_t s);
+                              const uint8_t* nbits, const uint8_t* ops, uint64_t count, const uint64_t* tile_off,
+                              const uint64_t* total, uint32_t* vals, uint64_t* result, hipStream_t s);
 
 constexpr int kStamps = 10;  // stamp slots per workgroup
 constexpr int32_t FSE_DEFERRED = 1;  // internal block status between the two decode passes

@@ -198,16 +198,28 @@ def bitstack_read(data, widths) -> tuple[list, int, bool]:
     return [int(x) for x in out[: nr.value]], nr.value, bool(fin.value)
 
 
-def bitstream_read(data, total_bits: int, widths) -> tuple[list, int, int]:
-    """BitStreamReader::new(slice, total_bits) + read(width) per field
-    (stream_reader.rs): (values read, number of successful reads, bits left)."""
+BITS_READ, BITS_PEEK, BITS_ADVANCE = 0, 1, 2  # FSE_BITS_* (include/fsehip.h)
+
+
+def bitstream_read(data, total_bits: int, widths, ops=None) -> tuple[list, int, int]:
+    """BitStreamReader::new(slice, total_bits) and one call per field
+    (stream_reader.rs:56-119): read(width), or with `ops` peek(width)
+    (BITS_PEEK) / advance_by(width) (BITS_ADVANCE, value 0).  Returns (values
+    of the steps that returned Ok, their number, available() after them)."""
     a = _buf(data)
     w = np.ascontiguousarray(widths, dtype=np.uint8)
     out = np.zeros(max(len(w), 1), dtype=np.uint32)
     nr = C.c_size_t(0)
     left = C.c_uint64(0)
-    check(load().bitstream_read(_p(a), len(a), total_bits, _p(w), len(w), _p(out), C.byref(nr), C.byref(left)),
-          "bitstream_read")
+    if ops is None:
+        check(load().bitstream_read(_p(a), len(a), total_bits, _p(w), len(w), _p(out), C.byref(nr), C.byref(left)),
+              "bitstream_read")
+    else:
+        o = np.ascontiguousarray(ops, dtype=np.uint8)
+        if len(o) != len(w):
+            raise ValueError("one op per field")
+        check(load().bitstream_read_ops(_p(a), len(a), total_bits, _p(w), _p(o), len(w), _p(out), C.byref(nr),
+                                        C.byref(left)), "bitstream_read_ops")
     return [int(x) for x in out[: nr.value]], nr.value, left.value
 
 
@@ -345,7 +357,8 @@ class BlockCodec:
         return cb["out"][s: s + ln].cpu().numpy().tobytes()
 
 
-__all__ = ["BlockCodec", "DecodeTable", "EncodeTable", "FseError", "Histogram", "NormHistogram", "bitstack_read",
-           "bitstack_write", "bitstream_read", "compress", "compress2", "compress2_log", "compress_nh", "decode_table_new",
-           "decompress", "decompress2", "encode_table_new", "histogram_count", "histogram_new", "norm_histogram_new",
-           "norm_histogram_read", "norm_histogram_write", "normalize", "normalize_optimal"]
+__all__ = ["BITS_ADVANCE", "BITS_PEEK", "BITS_READ", "BlockCodec", "DecodeTable", "EncodeTable", "FseError",
+           "Histogram", "NormHistogram", "bitstack_read", "bitstack_write", "bitstream_read", "compress", "compress2",
+           "compress2_log", "compress_nh", "decode_table_new", "decompress", "decompress2", "encode_table_new",
+           "histogram_count", "histogram_new", "norm_histogram_new", "norm_histogram_read", "norm_histogram_write",
+           "normalize", "normalize_optimal"]

@@ -160,6 +160,18 @@ int bitstack_read(const uint8_t* src, size_t n, const uint8_t* nbits, size_t cou
                   int* finished);
 int bitstream_read(const uint8_t* src, size_t n, uint64_t total_bits, const uint8_t* nbits, size_t count,
                    uint32_t* vals, size_t* n_read, uint64_t* bits_left);
+/* BitStreamReader with each field's call named (stream_reader.rs:56-119):
+ * ops[i] = FSE_BITS_READ (read), FSE_BITS_PEEK (peek: value, no advance) or
+ * FSE_BITS_ADVANCE (advance_by: advance, value 0).  Any of them fails past
+ * total_bits (UnexpectedEof) and stops the list: *n_done = steps that
+ * returned Ok, *bits_left = available() after them (finish(): the remaining
+ * slice starts at byte (total_bits - *bits_left) / 8, finish_byte() at the
+ * next byte boundary).  ops = NULL: all reads, as bitstream_read. */
+#define FSE_BITS_READ 0
+#define FSE_BITS_PEEK 1
+#define FSE_BITS_ADVANCE 2
+int bitstream_read_ops(const uint8_t* src, size_t n, uint64_t total_bits, const uint8_t* nbits, const uint8_t* ops,
+                       size_t count, uint32_t* vals, size_t* n_done, uint64_t* bits_left);
 
 /* ------------------------------------------------------------------------
  * (2) Batched device entry points
@@ -254,6 +266,11 @@ int fsehip_bitstack_read(const uint8_t* d_in, uint64_t n_bytes, const uint8_t* d
                          uint32_t* d_vals, uint64_t* d_result, fsehip_stream_t stream);
 int fsehip_bitstream_read(const uint8_t* d_in, uint64_t n_bytes, uint64_t total_bits, const uint8_t* d_nbits,
                           uint64_t count, uint32_t* d_vals, uint64_t* d_result, fsehip_stream_t stream);
+/* The same with per-field ops (FSE_BITS_READ / PEEK / ADVANCE, device
+ * pointer; NULL = all reads). */
+int fsehip_bitstream_read_ops(const uint8_t* d_in, uint64_t n_bytes, uint64_t total_bits, const uint8_t* d_nbits,
+                              const uint8_t* d_ops, uint64_t count, uint32_t* d_vals, uint64_t* d_result,
+                              fsehip_stream_t stream);
 
 /* histogram::count per block: d_counts[b*256 + s], d_table_len[b]. */
 int fsehip_histogram_blocks(const uint8_t* d_src, uint64_t n_total, uint32_t block_size, uint32_t* d_counts,

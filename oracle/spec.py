@@ -71,6 +71,26 @@ class Stack:
         return sum(b << i for i, b in enumerate(chunk))
 
 
+def stream_steps(data: bytes, total_bits: int, widths, ops):
+    """BitStreamReader (stream_reader.rs:16-119) driven by one call per
+    field: op 0 = read (peek then advance_by, 56-60), 1 = peek (82-114), 2 =
+    advance_by (67-75, no value: 0 here).  Bits are LSB-first, bytes past the
+    slice read as zero, and any call with bits_read + bits > total_bits fails
+    (UnexpectedEof), which ends the list.  Returns (values, calls that
+    returned Ok, available() after them)."""
+    if not data or (total_bits + 7) // 8 != len(data):
+        raise SpecError("BAD_ARG")  # the constructor's asserts (17-21)
+    v = int.from_bytes(data, "little")
+    pos, out = 0, []
+    for w, op in zip(widths, ops):
+        if pos + w > total_bits:
+            break
+        out.append(0 if op == 2 else (v >> pos) & ((1 << w) - 1))
+        if op != 1:
+            pos += w
+    return out, len(out), total_bits - pos
+
+
 # ---------------------------------------------------------------- histogram
 def histogram(data: bytes):
     """Histogram::new (histogram.rs:18-66) -> (counts, size, table_len)."""

@@ -198,6 +198,30 @@ def test_bitstream_read(torch_cuda):
     assert e.value.code == "BAD_ARG"
 
 
+def test_bitstream_peek_advance(torch_cuda):
+    """BitStreamReader's peek / advance_by / read mixed per field
+    (stream_reader.rs:56-119) against the spec model, including the failing
+    call at the end and finish()'s remaining bits."""
+    from oracle import spec
+    from entropy_coders_amd import BITS_ADVANCE, BITS_PEEK, FseError, bitstream_read
+
+    rng = np.random.default_rng(9)
+    for count in (1, 7, 200, 5000):
+        widths = rng.integers(1, 17, count).astype(np.uint8)
+        vals = rng.integers(0, 1 << 16, count, dtype=np.uint64) & ((1 << widths.astype(np.uint64)) - 1)
+        data, total = O.bits_write(vals, widths, False)
+        ops = rng.integers(0, 3, count).astype(np.uint8)
+        # a tail of calls that runs past total_bits
+        ops = np.append(ops, [BITS_PEEK, BITS_ADVANCE, 0]).astype(np.uint8)
+        w2 = np.append(widths, [16, 16, 16]).astype(np.uint8)
+        want = spec.stream_steps(bytes(data), total, w2.tolist(), ops.tolist())
+        got = bitstream_read(data, total, w2, ops)
+        assert got == (want[0], want[1], want[2]), count
+    with pytest.raises(FseError) as e:
+        bitstream_read(b"\x01", 8, [1], [3])  # unknown op
+    assert e.value.code == "BAD_ARG"
+
+
 def test_bitstack_device_batched(torch_cuda):
     """fsehip_bitstack_write / read on 3M device-resident fields against the
     oracle's writer."""
