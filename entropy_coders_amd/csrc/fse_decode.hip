@@ -19,6 +19,8 @@
 // L 5..11, 12, 13..15).  At LMAX = 15 the table (128 KiB) leaves no LDS for
 // the block image, so those blocks are read through a register window from
 // global memory.
+#include <type_traits>
+
 #include "fse_device.hpp"
 #include "fse_kernels.h"
 
@@ -797,53 +799,86 @@ __device__ __forceinline__ void lds_store_volatile(int32_t* p, int32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// The sidecar-less decoder's table in LDS, per block.  L <= 11 (COMPACT):
+// u16 entries nb | newState << 5 plus a u8 symbol array, 6 KiB instead of
+// 8 KiB, so 5 blocks fit a workgroup where 4 did; L = 12: the u32 entries of
+// dtable_blocks_kernel (nb | sym << 8 | newState << 18).  Either way the low
+// five bits are nb (nb <= 15, the next field starts at bit 5 or 8), so
+// v_bfe can take the entries themselves as width / offset operands, and
+// e >> SH is the byte offset of entry newState.
+template <bool COMPACT>
+struct RingTab {
+    static constexpr uint32_t SH = COMPACT ? 4u : 16u;  // e >> SH = newState * entry bytes
+    static constexpr uint32_t ESH = COMPACT ? 1u : 2u;  // log2 entry bytes
+    const uint8_t* ent;                                 // entries
+    const uint8_t* sym;                                 // COMPACT: symbols
+    __device__ __forceinline__ uint32_t entry_at(uint32_t a) const {  // a = byte offset
+        return COMPACT ? (uint32_t)*reinterpret_cast<const uint16_t*>(ent + a)
+                       : *reinterpret_cast<const uint32_t*>(ent + a);
+    }
+    __device__ __forceinline__ uint32_t sym_at(uint32_t a, uint32_t e) const {
+        return COMPACT ? (uint32_t)sym[a >> 1] : (e >> 8) & 0xFFu;
+    }
+    // by state index (end-of-block steps)
+    __device__ __forceinline__ uint32_t nb(uint32_t s) const { return entry_at(s << ESH) & 31u; }
+    __device__ __forceinline__ uint32_t symbol(uint32_t s) const { return sym_at(s << ESH, entry_at(s << ESH)); }
+    __device__ __forceinline__ uint32_t next_base(uint32_t s) const { return (entry_at(s << ESH) >> SH) >> ESH; }
+};
+
 // LdsChain over the ring.  NS = 2: a pair (<= 24 bits) per step; NS = 1:
 // one symbol (<= 12 bits).  The window [lo, lo + 64) covers the step's bits
 // and lo moves down by at most one word per step, so the upper word is
-// either the previous upper word or the previous lower one.
-template <int NS>
+// either the previous upper word or the previous lower one.  a0 / a1 are
+// the states' entry byte offsets.
+template <int NS, bool COMPACT>
 struct RingChain {
     static constexpr int32_t OFF = 12 * NS;
+    using Tab = RingTab<COMPACT>;
     int32_t pos, B;
     uint32_t whi, wlo, a0, a1;
     __device__ __forceinline__ void init(const uint32_t* ring, int32_t p, uint32_t s0, uint32_t s1) {
         pos = p;
-        a0 = s0 << 2;
-        a1 = s1 << 2;
+        a0 = s0 << Tab::ESH;
+        a1 = s1 << Tab::ESH;
         B = (p - OFF) & ~31;
         wlo = 0;
         whi = ring[((uint32_t)(B >> 5) + 1u) & RING_MASK];
     }
-    __device__ __forceinline__ uint32_t pair(const uint32_t* ring, const uint8_t* dtb) {
+    __device__ __forceinline__ uint32_t s0() const { return a0 >> Tab::ESH; }
+    __device__ __forceinline__ uint32_t s1() const { return a1 >> Tab::ESH; }
+    // one pair; returns sym0 | sym1 << 8
+    __device__ __forceinline__ uint32_t pair(const uint32_t* ring, const Tab& T) {
         const int32_t lo = (pos - OFF) & ~31;
         const uint32_t w0 = ring[(uint32_t)(lo >> 5) & RING_MASK];
-        const uint32_t e0 = *reinterpret_cast<const uint32_t*>(dtb + a0);
-        const uint32_t e1 = *reinterpret_cast<const uint32_t*>(dtb + a1);
+        const uint32_t e0 = T.entry_at(a0);
+        const uint32_t e1 = T.entry_at(a1);
+        const uint32_t y0 = T.sym_at(a0, e0), y1 = T.sym_at(a1, e1);
         const uint32_t w1 = lo == B ? whi : wlo;
-        pos -= (int32_t)((e0 + e1) & 0xFFu);
+        pos -= (int32_t)((e0 + e1) & 31u);
         const uint32_t x = (uint32_t)((((uint64_t)w1 << 32) | w0) >> (uint32_t)(pos - lo));
         B = lo;
         whi = w1;
         wlo = w0;
         const uint32_t v1 = __builtin_amdgcn_ubfe(x, 0u, e1);
         const uint32_t v0 = __builtin_amdgcn_ubfe(x, e1, e0);
-        a0 = (e0 >> 16) + (v0 << 2);
-        a1 = (e1 >> 16) + (v1 << 2);
-        return __builtin_amdgcn_perm(e1, e0, 0x0c0c0501u);  // sym0 | sym1 << 8
+        a0 = (e0 >> Tab::SH) + (v0 << Tab::ESH);
+        a1 = (e1 >> Tab::SH) + (v1 << Tab::ESH);
+        return y0 | (y1 << 8);
     }
-    // NS = 1: one symbol; returns its entry (symbol in bits 8-15)
-    __device__ __forceinline__ uint32_t step(const uint32_t* ring, const uint8_t* dtb) {
+    // NS = 1: one symbol; returns it
+    __device__ __forceinline__ uint32_t step(const uint32_t* ring, const Tab& T) {
         const int32_t lo = (pos - OFF) & ~31;
         const uint32_t w0 = ring[(uint32_t)(lo >> 5) & RING_MASK];
-        const uint32_t e = *reinterpret_cast<const uint32_t*>(dtb + a0);
+        const uint32_t e = T.entry_at(a0);
+        const uint32_t y = T.sym_at(a0, e);
         const uint32_t w1 = lo == B ? whi : wlo;
-        pos -= (int32_t)(e & 0xFFu);
+        pos -= (int32_t)(e & 31u);
         const uint32_t x = (uint32_t)((((uint64_t)w1 << 32) | w0) >> (uint32_t)(pos - lo));
         B = lo;
         whi = w1;
         wlo = w0;
-        a0 = (e >> 16) + (__builtin_amdgcn_ubfe(x, 0u, e) << 2);
-        return e;
+        a0 = (e >> Tab::SH) + (__builtin_amdgcn_ubfe(x, 0u, e) << Tab::ESH);
+        return y;
     }
 };
 
@@ -851,8 +886,10 @@ template <int LMAX, uint32_t K, int NS>
 __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
     static_assert(LMAX <= 12, "entry layout ns << 18: e >> 16 is the next entry's byte offset");
     static_assert(K >= 1 && K <= 64, "one decode lane per block");
+    constexpr bool COMPACT = LMAX <= 11;  // newState < 2^11: nb | ns << 5 fits 16 bits
     constexpr uint32_t TW = 1u << LMAX;
-    __shared__ __attribute__((aligned(16))) uint32_t tab_all[K * TW];
+    constexpr uint32_t TAB_BYTES = COMPACT ? 3u * TW : 4u * TW;  // per block
+    __shared__ __attribute__((aligned(16))) uint8_t tab_all[K * TAB_BYTES];
     __shared__ uint32_t ring_all[K * RING_WORDS];
     __shared__ int32_t ctl_all[K][2];  // [0] lowest word landed, [1] highest word the decoder may still read; INT32_MIN = stop
     __shared__ uint32_t any_nb[K];
@@ -874,11 +911,20 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
         if (info < 0) continue;
         const uint32_t nv = (1u << ((uint32_t)info >> 16)) >> 2;
         const uint4* t4 = reinterpret_cast<const uint4*>(P.dt + gb * (uint64_t)TW);
-        uint4* d4 = reinterpret_cast<uint4*>(tab_all + j * TW);
+        uint8_t* tb = tab_all + j * TAB_BYTES;
         uint32_t nbor = 0;
         for (uint32_t i = tid; i < nv; i += 128u) {
             const uint4 q = t4[i];
-            d4[i] = q;
+            if (COMPACT) {  // nb | ns << 5 (ns = e >> 18) and the symbols, 4 entries at a time
+                auto c16 = [](uint32_t e) { return (e & 0xFu) | ((e >> 13) & ~31u); };
+                reinterpret_cast<uint2*>(tb)[i] =
+                    make_uint2(c16(q.x) | (c16(q.y) << 16), c16(q.z) | (c16(q.w) << 16));
+                reinterpret_cast<uint32_t*>(tb + 2u * TW)[i] =
+                    __builtin_amdgcn_perm(__builtin_amdgcn_perm(q.w, q.z, 0x0c0c0501u),
+                                          __builtin_amdgcn_perm(q.y, q.x, 0x0c0c0501u), 0x05040100u);
+            } else {
+                reinterpret_cast<uint4*>(tb)[i] = q;
+            }
             nbor |= (q.x | q.y | q.z | q.w) & 0xFFu;
         }
         if (nbor) atomicOr(&any_nb[j], 1u);
@@ -936,7 +982,7 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
     if (lane >= K || gb >= P.n_blocks) return;
 
     // wave 0, lane j < K: the decoder of block gb0 + j
-    uint32_t* const tab = tab_all + lane * TW;
+    const RingTab<COMPACT> T{tab_all + lane * TAB_BYTES, tab_all + lane * TAB_BYTES + 2u * TW};
     const uint32_t* const ring = ring_all + lane * RING_WORDS;
     int32_t* const ctl = ctl_all[lane];
     const int32_t info = P.dtinfo[gb];
@@ -963,7 +1009,6 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
         if (top - NS * (int32_t)L < hdr_bits) err = FSE_ERR_TOO_SHORT;  // lib.rs:197 / 224-225 unwrap
     }
     if (err == FSE_OK) {
-        const uint8_t* dtb = reinterpret_cast<const uint8_t*>(tab);
         int32_t avail = nw;
         auto wait_words = [&](int32_t wlow) {  // words >= max(wlow, 0) have landed
             wlow = max(wlow, 0);
@@ -980,7 +1025,7 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
         wait_words((top - NS * (int32_t)L) >> 5);
         const uint32_t s0i = bits_at(top - (int32_t)L) & ((1u << L) - 1u);
         const uint32_t s1i = NS == 2 ? bits_at(top - 2 * (int32_t)L) & ((1u << L) - 1u) : 0u;
-        RingChain<NS> c;
+        RingChain<NS, COMPACT> c;
         c.init(ring, top - NS * (int32_t)L, s0i, s1i);
         const uint32_t I = P.ckpt_interval;
         uint64_t* rec = (P.sidecar_out && I) ? P.sidecar_out + gb * P.ckpt_per_block : nullptr;
@@ -994,47 +1039,54 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
                 next_ck = ck < P.ckpt_per_block ? next_ck + I : 0xFFFFFFFFu;
             }
         };
-        auto record = [&]() { record_at(c.pos, c.a0 >> 2, c.a1 >> 2); };
-        // bulk: 16 output bytes (8 pairs / 16 symbols, <= 16L bits) without end checks
-        while (o + 18u < lim && c.pos - hdr_bits >= 16 * (int32_t)L) {
-            wait_words((c.pos - NS * 12 - 16 * (int32_t)L) >> 5);
-            uint32_t w[4];
-            if constexpr (NS == 2) {
+        // bulk: 16 output bytes (8 pairs / 16 symbols, <= 16L bits) without end
+        // checks; the checkpoint compare is compiled in only when recording
+        auto bulk = [&](auto rec_on) {
+            constexpr bool REC = decltype(rec_on)::value;
+            auto record = [&]() {
+                if (REC) record_at(c.pos, c.s0(), c.s1());
+            };
+            while (o + 18u < lim && c.pos - hdr_bits >= 16 * (int32_t)L) {
+                wait_words((c.pos - NS * 12 - 16 * (int32_t)L) >> 5);
+                uint32_t w[4];
+                if constexpr (NS == 2) {
 #pragma unroll
-                for (uint32_t j = 0; j < 8u; j += 2u) {
-                    record();
-                    const uint32_t lo = c.pair(ring, dtb);
-                    ++pidx;
-                    record();
-                    const uint32_t hi = c.pair(ring, dtb);
-                    ++pidx;
-                    w[j >> 1] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
-                }
-            } else {
-#pragma unroll
-                for (uint32_t j = 0; j < 4u; ++j) {
-                    uint32_t e[4];
-#pragma unroll
-                    for (uint32_t q = 0; q < 4u; ++q) {
+                    for (uint32_t j = 0; j < 8u; j += 2u) {
                         record();
-                        e[q] = c.step(ring, dtb);
+                        const uint32_t lo = c.pair(ring, T);
                         ++pidx;
+                        record();
+                        const uint32_t hi = c.pair(ring, T);
+                        ++pidx;
+                        w[j >> 1] = lo | (hi << 16);
                     }
-                    w[j] = __builtin_amdgcn_perm(__builtin_amdgcn_perm(e[3], e[2], 0x0c0c0501u),
-                                                 __builtin_amdgcn_perm(e[1], e[0], 0x0c0c0501u), 0x05040100u);
+                } else {
+#pragma unroll
+                    for (uint32_t j = 0; j < 4u; ++j) {
+                        uint32_t y = 0;
+#pragma unroll
+                        for (uint32_t q = 0; q < 4u; ++q) {
+                            record();
+                            y |= c.step(ring, T) << (8u * q);
+                            ++pidx;
+                        }
+                        w[j] = y;
+                    }
                 }
+                *reinterpret_cast<uint4*>(out + o) = make_uint4(w[0], w[1], w[2], w[3]);
+                o += 16;
+                lds_store_volatile(&ctl[1], (c.pos - NS * 12) >> 5);
             }
-            *reinterpret_cast<uint4*>(out + o) = make_uint4(w[0], w[1], w[2], w[3]);
-            o += 16;
-            lds_store_volatile(&ctl[1], (c.pos - NS * 12) >> 5);
-        }
+        };
+        if (rec) bulk(std::true_type{});
+        else bulk(std::false_type{});
         // the tail reads words <= pos/32 + 1, and it ends within 16L bits
         // (bulk stopped by the position) or within 18 steps (stopped by the
         // output limit): wait for just those words, the loader cannot pass
         // the ring's words above what the decoder still reads
         lds_store_volatile(&ctl[1], (c.pos >> 5) + 1);
         wait_words(max(hdr_bits, c.pos - 20 * (int32_t)L) >> 5);
-        uint32_t s0 = c.a0 >> 2, s1 = c.a1 >> 2;
+        uint32_t s0 = c.s0(), s1 = c.s1();
         int32_t pos = c.pos;
         auto pop = [&](uint32_t nb) -> uint32_t {
             pos -= (int32_t)nb;
@@ -1046,51 +1098,51 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
             for (;; ++pidx) {
                 record_at(pos, s0, s1);
                 if (known && o + 2u >= n) {
-                    if (o < n) out[o++] = (uint8_t)dte_sym(tab[s0]);
-                    if (o < n) out[o++] = (uint8_t)dte_sym(tab[s1]);
+                    if (o < n) out[o++] = (uint8_t)T.symbol(s0);
+                    if (o < n) out[o++] = (uint8_t)T.symbol(s1);
                     break;
                 }
-                const uint32_t e0 = tab[s0];
-                uint32_t nb = dte_nb(e0);
+                uint32_t nb = T.nb(s0);
                 if (pos - (int32_t)nb < hdr_bits) {  // decoder 0 cannot read: lib.rs:242-243
                     if (o + 2u > lim) { err = full; break; }
-                    out[o++] = (uint8_t)dte_sym(e0);
-                    out[o++] = (uint8_t)dte_sym(tab[s1]);
+                    out[o++] = (uint8_t)T.symbol(s0);
+                    out[o++] = (uint8_t)T.symbol(s1);
                     break;
                 }
-                s0 = Dte<LMAX>::ns(e0) + pop(nb);
+                const uint32_t y0 = T.symbol(s0);
+                s0 = T.next_base(s0) + pop(nb);
                 if (o >= lim) { err = full; break; }
-                out[o++] = (uint8_t)dte_sym(e0);
-                const uint32_t e1 = tab[s1];
-                nb = dte_nb(e1);
+                out[o++] = (uint8_t)y0;
+                nb = T.nb(s1);
                 if (pos - (int32_t)nb < hdr_bits) {  // decoder 1 cannot read: lib.rs:235-239
                     if (o + 2u > lim) { err = full; break; }
-                    out[o++] = (uint8_t)dte_sym(e1);
-                    out[o++] = (uint8_t)dte_sym(tab[s0]);
+                    out[o++] = (uint8_t)T.symbol(s1);
+                    out[o++] = (uint8_t)T.symbol(s0);
                     break;
                 }
-                s1 = Dte<LMAX>::ns(e1) + pop(nb);
+                const uint32_t y1 = T.symbol(s1);
+                s1 = T.next_base(s1) + pop(nb);
                 if (o >= lim) { err = full; break; }
-                out[o++] = (uint8_t)dte_sym(e1);
+                out[o++] = (uint8_t)y1;
             }
             if (err == FSE_OK && known && o != n) err = FSE_ERR_LENGTH_MISMATCH;
         } else {
             // tail: symbol by symbol (lib.rs:198-208), then Decoder::finish
             for (;; ++pidx) {
                 record_at(pos, s0, 0u);
-                const uint32_t e = tab[s0];
-                const uint32_t nb = dte_nb(e);
+                const uint32_t nb = T.nb(s0);
                 if (pos - (int32_t)nb < hdr_bits) break;  // decode_symbol -> None
                 if (o >= lim) {  // nb == 0 forever: a probability-1 symbol never ends in the reference
                     err = nb == 0 ? FSE_ERR_SINGLE_SYMBOL : FSE_ERR_DST_TOO_SMALL;
                     break;
                 }
-                s0 = Dte<LMAX>::ns(e) + pop(nb);
-                out[o++] = (uint8_t)dte_sym(e);
+                const uint32_t y = T.symbol(s0);
+                s0 = T.next_base(s0) + pop(nb);
+                out[o++] = (uint8_t)y;
             }
             if (err == FSE_OK) {
                 if (o >= lim) err = FSE_ERR_DST_TOO_SMALL;
-                else out[o++] = (uint8_t)dte_sym(tab[s0]);  // Decoder::finish (lib.rs:208)
+                else out[o++] = (uint8_t)T.symbol(s0);  // Decoder::finish (lib.rs:208)
             }
             if (known && (err == FSE_ERR_DST_TOO_SMALL || (err == FSE_OK && o != n))) err = FSE_ERR_LENGTH_MISMATCH;
         }
@@ -1108,12 +1160,12 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
     if (!P.dt || !P.dtinfo) return hipErrorInvalidValue;
     if (!P.sidecar) {  // serial: sidecar-less blocks, reference-mode host streams, sidecar recording
         if (P.nstates == 1) {
-            if (lmax <= 11) hipLaunchKernelGGL((serial_ring_kernel<11, 4, 1>), dim3((P.n_blocks + 3u) / 4u), dim3(128), 0, stream, P);
+            if (lmax <= 11) hipLaunchKernelGGL((serial_ring_kernel<11, 5, 1>), dim3((P.n_blocks + 4u) / 5u), dim3(128), 0, stream, P);
             else if (lmax <= 12) hipLaunchKernelGGL((serial_ring_kernel<12, 2, 1>), dim3((P.n_blocks + 1u) / 2u), dim3(128), 0, stream, P);
             else hipLaunchKernelGGL((decode1_serial_kernel<15>), g, dim3(64), 0, stream, P);
         } else {
-            // 4 (L <= 11) or 2 (L = 12) blocks per workgroup: 16 / 8 chains per CU (LDS-bound)
-            if (lmax <= 11) hipLaunchKernelGGL((serial_ring_kernel<11, 4, 2>), dim3((P.n_blocks + 3u) / 4u), dim3(128), 0, stream, P);
+            // 5 (L <= 11, compact tables) or 2 (L = 12) blocks per workgroup: 20 / 8 chains per CU (LDS-bound)
+            if (lmax <= 11) hipLaunchKernelGGL((serial_ring_kernel<11, 5, 2>), dim3((P.n_blocks + 4u) / 5u), dim3(128), 0, stream, P);
             else if (lmax <= 12) hipLaunchKernelGGL((serial_ring_kernel<12, 2, 2>), dim3((P.n_blocks + 1u) / 2u), dim3(128), 0, stream, P);
             else hipLaunchKernelGGL((serial2_decode_kernel<15>), g, dim3(64), 0, stream, P);
         }
