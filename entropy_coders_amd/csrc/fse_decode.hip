@@ -538,8 +538,16 @@ __global__ __launch_bounds__(64) void dtable_blocks_kernel(DtParams P) {
 template <int LMAX>
 __global__ __launch_bounds__(64) void decode1_serial_kernel(DecParams P) {
     const uint64_t gb = blockIdx.x;
-    if (gb >= P.n_blocks || threadIdx.x != 0) return;
+    if (gb >= P.n_blocks) return;
     const int32_t info = P.dtinfo[gb];
+    // single-symbol table (every nb 0): the whole wave scans it
+    uint32_t nbor = 0;
+    if (info >= 0) {
+        const uint32_t* t = P.dt + gb * (uint64_t)(1u << LMAX);
+        for (uint32_t i = threadIdx.x; i < (1u << ((uint32_t)info >> 16)); i += 64u) nbor |= t[i] & 0xFFu;
+    }
+    const bool single = __ballot(nbor != 0u) == 0ull;
+    if (threadIdx.x != 0) return;
     if (info < 0) {
         P.status[gb] = info;
         if (P.out_len) P.out_len[gb] = 0;
@@ -565,6 +573,7 @@ __global__ __launch_bounds__(64) void decode1_serial_kernel(DecParams P) {
         uint32_t s = br.pop(L);
         br.refill();
         for (;;) {
+            if (known && single && o + 1u >= n) break;  // raw length ends a single-symbol block
             const uint32_t e = dt[s];
             const uint32_t nb = dte_nb(e);
             if (br.pos - (int32_t)nb < hdr_bits) break;  // decode_symbol -> None
@@ -1127,8 +1136,11 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
             }
             if (err == FSE_OK && known && o != n) err = FSE_ERR_LENGTH_MISMATCH;
         } else {
-            // tail: symbol by symbol (lib.rs:198-208), then Decoder::finish
+            // tail: symbol by symbol (lib.rs:198-208), then Decoder::finish.  A
+            // single-symbol table never fails a read (the reference loops
+            // forever); with the raw length known it ends at n - 1 symbols.
             for (;; ++pidx) {
+                if (known && single && o + 1u >= n) break;
                 record_at(pos, s0, 0u);
                 const uint32_t nb = T.nb(s0);
                 if (pos - (int32_t)nb < hdr_bits) break;  // decode_symbol -> None

@@ -1,0 +1,95 @@
+"""Seeded randomized parity sweep of the batched path against the oracle:
+block sizes, ragged lengths, distributions (LUT-skewed, uniform subsets,
+sparse alphabets, occasional degenerate blocks), table logs 5..15, both
+formats (fse_compress2 / fse_compress) and checkpoint intervals.  Every
+block's bytes and status are compared with the oracle, and each batch is
+decoded through every route: the sidecar segments, the sidecar-less serial
+decoder, and the serial decoder that rebuilds the sidecar."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def _block(rng, n):
+    kind = rng.integers(0, 6)
+    if kind == 0:  # the bench's LUT generator at a random skew
+        return O.generate(0, float(rng.uniform(0.03, 0.9)), int(rng.integers(1 << 30)), 0, n)
+    if kind == 1:  # uniform over a random subset of the alphabet
+        alpha = rng.choice(256, size=int(rng.integers(2, 257)), replace=False).astype(np.uint8)
+        return alpha[rng.integers(0, len(alpha), n)]
+    if kind == 2:  # sparse alphabet with long zero runs in the header, skewed weights
+        alpha = np.sort(rng.choice(256, size=int(rng.integers(2, 9)), replace=False)).astype(np.uint8)
+        w = rng.random(len(alpha)) ** 3 + 1e-3
+        return alpha[rng.choice(len(alpha), size=n, p=w / w.sum())]
+    if kind == 3:  # geometric symbols (C1's shape)
+        return np.minimum(rng.geometric(float(rng.uniform(0.2, 0.8)), n) - 1, 255).astype(np.uint8)
+    if kind == 4:  # degenerate: a single symbol, all zeros (a reference panic) or two symbols
+        return [np.full(n, int(rng.integers(1, 256)), np.uint8), np.zeros(n, np.uint8),
+                (rng.random(n) < 0.001).astype(np.uint8) * 200][int(rng.integers(0, 3))]
+    return rng.integers(0, 256, n).astype(np.uint8)  # near-uniform full alphabet
+
+
+@pytest.mark.parametrize("case", range(48))
+def test_random_batches(torch_cuda, case):
+    torch = torch_cuda
+    from entropy_coders_amd import BlockCodec
+    from entropy_coders_amd._lib import STATUS
+
+    rng = np.random.default_rng(0xF0220 + case)
+    nstates = int(rng.choice([1, 2]))
+    block = int(rng.choice([512, 1040, 4096, 20000, 65536]))
+    nblocks = int(rng.integers(1, 9))
+    last = int(rng.integers(2, block + 1))
+    table_log = 0 if nstates == 1 else int(rng.choice([0, 0, 5, 7, 9, 11, 12, 13, 15]))
+    ckpt = int(rng.choice([0, 64, 128, 256]))
+    sizes = [block] * (nblocks - 1) + [last]
+    blocks = [_block(rng, s) for s in sizes]
+    host = np.concatenate(blocks)
+    n = len(host)
+
+    codec = BlockCodec(block_size=block, table_log=table_log, ckpt_interval=ckpt, nstates=nstates)
+    src = torch.from_numpy(host).cuda()
+    cb = codec.compress(src)
+    routes = [("serial", codec.decompress(cb, use_sidecar=False))]
+    if ckpt:
+        routes.append(("sidecar", codec.decompress(cb)))
+        rebuilt = codec.build_sidecar(cb)
+        routes.append(("rebuild", rebuilt[::2]))
+    torch.cuda.synchronize()
+    est = cb["status"].cpu().numpy()
+    spb = codec.side_per_block
+    for b, s in enumerate(blocks):
+        what = (case, b, nstates, block, table_log, ckpt)
+        try:
+            if nstates == 2:
+                want, wbits = O.compress2(s, table_log or None)
+            else:
+                want, wbits = O.compress(s)
+        except O.OracleError as e:
+            assert STATUS.get(int(est[b])) == e.code, what
+            for name, (out, st) in routes:
+                assert int(st[b]) != 0, (name, what)
+            continue
+        assert est[b] == 0, (what, STATUS.get(int(est[b])))
+        assert codec.block_bytes(cb, b) == want, what
+        assert int(cb["payload_bits"][b]) == wbits, what
+        lo = b * block
+        for name, (out, st) in routes:
+            assert int(st[b]) == 0, (name, what, STATUS.get(int(st[b])))
+            assert np.array_equal(out[lo: lo + len(s)].cpu().numpy(), s), (name, what)
+        if ckpt:
+            side = rebuilt[1]
+            assert torch.equal(side[b * spb: (b + 1) * spb], cb["sidecar"][b * spb: (b + 1) * spb]), what
+    assert n == sum(sizes)
