@@ -28,6 +28,11 @@ def _inputs():
     yield O.generate(0, 0.05, 24, 0, 65536)        # normalize_slow at low L
     yield O.generate(1, 0.5, 25, 0, 1001)          # geometric, short
     yield np.frombuffer(bytes([0, 5, 5, 200] * 40 + [255]), dtype=np.uint8)  # sparse alphabet, long zero runs
+    from test_gpu_fuzz import _block  # seeded random distributions and lengths
+
+    rng = np.random.default_rng(0xB10C)
+    for _ in range(8):
+        yield _block(rng, int(rng.integers(2, 65537)))
 
 
 def _norm_eq(a, b):

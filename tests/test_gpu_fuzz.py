@@ -93,3 +93,28 @@ def test_random_batches(torch_cuda, case):
             side = rebuilt[1]
             assert torch.equal(side[b * spb: (b + 1) * spb], cb["sidecar"][b * spb: (b + 1) * spb]), what
     assert n == sum(sizes)
+
+
+@pytest.mark.parametrize("case", range(16))
+def test_random_host_calls(torch_cuda, case):
+    """The reference-shaped host entry points on random blocks: fse_compress2
+    (and with an explicit table log, clamped as Histogram::normalize does),
+    fse_decompress2, fse_compress, fse_decompress, against the oracle."""
+    from entropy_coders_amd import FseError, compress, compress2, compress2_log, decompress, decompress2
+
+    rng = np.random.default_rng(0xA110 + case)
+    s = _block(rng, int(rng.integers(2, 65537)))
+    L = int(rng.integers(0, 21))
+    for enc, ref, dec in ((compress2, O.compress2, decompress2), (compress, O.compress, decompress),
+                          (lambda x: compress2_log(x, L), lambda x: O.compress2(x, L), decompress2)):
+        try:
+            want, wbits = ref(s)
+        except O.OracleError as e:
+            with pytest.raises(FseError) as g:
+                enc(s)
+            assert g.value.code == e.code, (case, L)
+            continue
+        got, bits = enc(s)
+        assert got == want and bits == wbits, (case, L)
+        if len(set(s.tolist())) > 1:  # a single-symbol stream never ends in the reference
+            assert dec(got) == s.tobytes(), (case, L)
