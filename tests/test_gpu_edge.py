@@ -187,7 +187,7 @@ def test_corrupt_blocks_fail_cleanly(torch_cuda, use_sidecar):
 
 @pytest.mark.parametrize("table_log,n_blocks", [(0, 1), (0, 3), (0, 5), (11, 7), (12, 1), (12, 3)])
 def test_sidecar_less_partial_groups(torch_cuda, table_log, n_blocks):
-    """The sidecar-less decoder packs K blocks into one workgroup (4 at
+    """The sidecar-less decoder packs K blocks into one workgroup (5 at
     L <= 11, 2 at L = 12), one decode lane each: block counts that leave a
     group part-empty, and a ragged last block, must decode exactly and
     rebuild the encoder's sidecar."""
@@ -207,3 +207,54 @@ def test_sidecar_less_partial_groups(torch_cuda, table_log, n_blocks):
     assert int(st.abs().max()) == 0 and int(st2.abs().max()) == 0
     assert torch.equal(out, src) and torch.equal(o2, src)
     assert torch.equal(side2, cb["sidecar"])
+
+
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("nstates", [2, 1])
+def test_random_corruption_never_hangs(torch_cuda, seed, nstates):
+    """Random damage (payload bytes, header bytes, lengths up to the slot,
+    the marker byte) on 40 blocks at once, decoded by every route: each block
+    ends with a status or garbage bytes inside its own output; no fault, no
+    hang (the serial decoder's loader wave and decode lanes must always
+    release each other), no write past the output."""
+    torch = torch_cuda
+    from entropy_coders_amd import BlockCodec
+
+    rng = np.random.default_rng(0xC0DE + seed)
+    block, nb = 4096, 40
+    codec = BlockCodec(block_size=block, ckpt_interval=64, nstates=nstates)
+    src = codec.generate(0, float(rng.uniform(0.05, 0.8)), int(rng.integers(1 << 30)), nb * block)
+    cb = codec.compress(src)
+    torch.cuda.synchronize()
+    slots = cb["out"].cpu().numpy().copy()
+    lens = cb["comp_len"].cpu().numpy().copy()
+    side = cb["sidecar"].cpu().numpy().copy()
+    sb = codec.slot_bytes
+    for b in range(nb):
+        base, ln = b * sb, int(lens[b])
+        for _ in range(int(rng.integers(0, 4))):
+            what = int(rng.integers(0, 5))
+            if what == 0:
+                slots[base + int(rng.integers(0, ln))] ^= np.uint8(1 << int(rng.integers(0, 8)))
+            elif what == 1:
+                slots[base: base + 4] = rng.integers(0, 256, 4, dtype=np.uint8)
+            elif what == 2:
+                lens[b] = int(rng.integers(1, sb + 1))
+            elif what == 3:
+                slots[base + ln - 1] = np.uint8(rng.integers(0, 256))
+            else:
+                side[b * codec.side_per_block + int(rng.integers(0, codec.side_per_block))] ^= np.int64(
+                    int(rng.integers(1, 1 << 40)))
+    cb["out"] = torch.from_numpy(slots).to(codec.device)
+    cb["comp_len"] = torch.from_numpy(lens).to(codec.device)
+    cb["sidecar"] = torch.from_numpy(side).to(codec.device)
+    for use_sidecar in (True, False):
+        buf = torch.full((nb * block + 4096,), 0x5A, dtype=torch.uint8, device=codec.device)
+        st = torch.full((nb,), 7, dtype=torch.int32, device=codec.device)
+        codec.decompress_into(cb, buf[: nb * block], st, use_sidecar=use_sidecar)
+        torch.cuda.synchronize()
+        assert bool((buf[nb * block:] == 0x5A).all()), "write past the output"
+        assert int(st.max()) <= 0, "a block without a status"
+    out, side2, st2 = codec.build_sidecar(cb)
+    torch.cuda.synchronize()
+    assert int(st2.max()) <= 0
