@@ -532,6 +532,8 @@ int fse_compress2_log(const uint8_t* src, size_t n, uint32_t table_log, uint8_t*
 // Host block decode (reference mode: the raw length is not in the format):
 // the block's table (stride 15, any L) and the serial decoder with the
 // reference's own termination within the caller's capacity.
+constexpr uint32_t LOG_MIN_HOST = 5;  // TABLE_LOG_MIN (lib.rs:9)
+
 static int decompress_one(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, size_t* dst_len,
                           uint32_t nstates) {
     if (!dst_len || *dst_len > dst_cap) return FSE_ERR_BAD_ARG;
@@ -543,16 +545,21 @@ static int decompress_one(const uint8_t* src, size_t n, uint8_t* dst, size_t dst
     uint8_t* d_in = g_stage.get(0, padded);
     uint8_t* d_out = g_stage.get(1, std::max<uint64_t>(cap64, 16));
     uint8_t* d_meta = g_stage.get(2, sizeof(Meta));
-    uint8_t* d_dt = g_stage.get(3, fsehip_dtable_bytes(15) + 16);
+    // the header's first field is the table log (histogram.rs:438: read(4) +
+    // 5): size the tables and pick the kernels by it (the L <= 11 / 12
+    // kernels keep the table in LDS; a bad header fails the parse either way)
+    const uint32_t Lh = (uint32_t)(src[0] & 15u) + LOG_MIN_HOST;
+    const uint32_t mtl = Lh <= 11u ? 11u : Lh <= 12u ? 12u : 15u;
+    uint8_t* d_dt = g_stage.get(3, fsehip_dtable_bytes(mtl) + 16);
     if (!d_in || !d_out || !d_meta || !d_dt) return FSE_ERR_HIP;
     if (hipMemset(d_in, 0, padded) != hipSuccess) return FSE_ERR_HIP;
     if (hipMemcpy(d_in, src, n, hipMemcpyHostToDevice) != hipSuccess) return FSE_ERR_HIP;
     Meta* m = reinterpret_cast<Meta*>(d_meta);
     Meta h0{(uint32_t)n, 0, 0, 0};
     if (hipMemcpy(d_meta, &h0, sizeof(Meta), hipMemcpyHostToDevice) != hipSuccess) return FSE_ERR_HIP;
-    fsehip_params p{0, 0, 0, 15, nstates};
+    fsehip_params p{0, 0, 0, mtl, nstates};
     uint32_t* dt = reinterpret_cast<uint32_t*>(d_dt);
-    int32_t* info = reinterpret_cast<int32_t*>(d_dt + fsehip_dtable_bytes(15));
+    int32_t* info = reinterpret_cast<int32_t*>(d_dt + fsehip_dtable_bytes(mtl));
     int rc = fsehip_build_dtables(&p, d_in, padded, &m->comp_len, 1, dt, info, nullptr);
     if (rc) return rc;
     rc = decompress_impl(&p, d_in, padded, &m->comp_len, nullptr, d_out, 0, nullptr, &m->status, &m->payload_bits,
