@@ -229,3 +229,28 @@ def test_checkpoints1_consistent():
         bp, s0 = O.checkpoints1(comp, iv)
         assert len(bp) == (n - 1) // iv + 1
         assert np.all(np.diff(bp.astype(np.int64)) < 0)
+
+
+@pytest.mark.parametrize("case", range(40))
+def test_oracle_matches_spec_random(case):
+    """The two independent restatements agree on seeded random blocks (the
+    fuzz generator's distributions, lengths up to 3 KiB, table logs 5..15,
+    both formats), including the error statuses and the decode."""
+    from test_gpu_fuzz import _block
+
+    rng = np.random.default_rng(0x5BEC + case)
+    src = _block(rng, int(rng.integers(2, 3073))).tobytes()
+    log2 = [None, 5, 8, 11, 12, 15][int(rng.integers(0, 6))]
+    for enc_o, enc_s, dec_s in ((lambda b: O.compress2(b, log2), lambda b: S.compress2(b, log2), S.decompress2),
+                                (O.compress, S.compress, S.decompress)):
+        try:
+            want = enc_s(src)
+        except S.SpecError as e:
+            with pytest.raises(O.OracleError) as ei:
+                enc_o(src)
+            assert ei.value.code == e.code, case
+            continue
+        got = enc_o(src)
+        assert got == want, case
+        if len(set(src)) > 1:
+            assert dec_s(want[0]) == src, case
