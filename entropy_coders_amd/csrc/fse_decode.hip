@@ -807,6 +807,17 @@ __device__ __forceinline__ void lds_store_volatile(int32_t* p, int32_t v) {
     __asm__ __volatile__("" ::: "memory");
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+// The ring handoff proper: the loader publishes "landed" with release
+// semantics after its ring writes, the decoder reads it with acquire (only
+// on its slow path, when the cached value is not low enough).  The
+// decoder's "still needed" hints stay relaxed: a stale value is a higher
+// one, which only makes the loader wait.
+__device__ __forceinline__ int32_t lds_load_acquire(int32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_store_release(int32_t* p, int32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
 // The sidecar-less decoder's table in LDS, per block.  L <= 11 (COMPACT):
 // u16 entries nb | newState << 5 plus a u8 symbol array, 6 KiB instead of
@@ -979,7 +990,7 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
                         ring_all[j * RING_WORDS +
                                  ((uint32_t)((k[j] - q) * (int32_t)RING_CHUNK + (int32_t)lane) & RING_MASK)] = v[q];
                 k[j] = k1;
-                if (lane == 0) lds_store_volatile(&ctl_all[j][0], (k1 + 1) * (int32_t)RING_CHUNK);
+                if (lane == 0) lds_store_release(&ctl_all[j][0], (k1 + 1) * (int32_t)RING_CHUNK);
                 if (k1 < 0) act &= ~(1u << j);
                 moved = true;
             }
@@ -1022,7 +1033,7 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
         auto wait_words = [&](int32_t wlow) {  // words >= max(wlow, 0) have landed
             wlow = max(wlow, 0);
             while (avail > wlow) {
-                avail = lds_load_volatile(&ctl[0]);
+                avail = lds_load_acquire(&ctl[0]);
                 if (avail > wlow) __builtin_amdgcn_s_sleep(1);
             }
         };
