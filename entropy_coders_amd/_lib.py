@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(HERE, os.environ.get("FSEHIP_LIB", "libfsehip.so"))
 EXPORTS = (
     "fse_compress2", "fse_compress2_log", "fse_decompress2", "histogram_count",
     "fsehip_slot_bytes", "fsehip_sidecar_per_block", "fsehip_compress_blocks",
-    "fsehip_decompress_blocks", "fsehip_build_sidecar", "fsehip_histogram_blocks",
+    "fsehip_decompress_blocks", "fsehip_build_sidecar", "fsehip_decompress_streams", "fsehip_histogram_blocks",
     "fsehip_generate", "fsehip_device_count", "fsehip_version",
     "fsehip_pack_blocks", "fsehip_unpack_blocks",
     "fsehip_dtable_bytes", "fsehip_build_dtables", "fsehip_decompress_blocks_dt",
@@ -109,6 +109,7 @@ def load() -> C.CDLL:
     lib.fsehip_compress_blocks.argtypes = [C.POINTER(Params), P, u64, P, u64, P, P, P, P, P]
     lib.fsehip_decompress_blocks.argtypes = [C.POINTER(Params), P, u64, P, P, P, u64, P, P]
     lib.fsehip_build_sidecar.argtypes = [C.POINTER(Params), P, u64, P, P, u64, P, P, P]
+    lib.fsehip_decompress_streams.argtypes = [C.c_uint32, C.c_uint32, P, u64, P, C.c_uint32, P, C.c_uint32, P, P, P]
     lib.fsehip_dtable_bytes.argtypes = [u32]
     lib.fsehip_dtable_bytes.restype = u64
     lib.fsehip_build_dtables.argtypes = [C.POINTER(Params), P, u64, P, u32, P, P, P]

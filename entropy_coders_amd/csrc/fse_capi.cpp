@@ -399,11 +399,8 @@ extern "C++" {
 // workspace, then `run(dt, info)` enqueues the decode on them; both under
 // the workspace lock.
 template <class Run>
-static int with_dtables(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes, const uint32_t* d_comp_len,
-                        uint64_t n_total, fsehip_stream_t stream, Run run) {
-    const uint32_t bs = p->block_size ? p->block_size : kDefaultBlock;
-    if (bs > kMaxBlock) return FSE_ERR_UNSUPPORTED;
-    const uint64_t n_blocks = (n_total + bs - 1) / bs;
+static int with_dtables_n(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes, const uint32_t* d_comp_len,
+                          uint64_t n_blocks, fsehip_stream_t stream, Run run) {
     if (n_blocks > 0xFFFFFFFFull) return FSE_ERR_BAD_ARG;
     if (!device_ok()) return FSE_ERR_NO_DEVICE;
     Lease lease(stream);
@@ -412,6 +409,13 @@ static int with_dtables(const fsehip_params* p, const uint8_t* d_in, uint64_t sl
     if (!dt || !info) return FSE_ERR_HIP;
     int rc = fsehip_build_dtables(p, d_in, slot_bytes, d_comp_len, (uint32_t)n_blocks, dt, info, stream);
     return rc != FSE_OK ? rc : run(dt, info);
+}
+template <class Run>
+static int with_dtables(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes, const uint32_t* d_comp_len,
+                        uint64_t n_total, fsehip_stream_t stream, Run run) {
+    const uint32_t bs = p->block_size ? p->block_size : kDefaultBlock;
+    if (bs > kMaxBlock) return FSE_ERR_UNSUPPORTED;
+    return with_dtables_n(p, d_in, slot_bytes, d_comp_len, (n_total + bs - 1) / bs, stream, run);
 }
 }  // extern "C++"
 
@@ -440,6 +444,38 @@ int fsehip_build_sidecar(const fsehip_params* p, const uint8_t* d_in, uint64_t s
         return decompress_impl(p, d_in, slot_bytes, d_comp_len, nullptr, d_out, n_total, d_sidecar_out, d_status,
                                nullptr, 0, stream, dt, info);
     });
+}
+
+int fsehip_decompress_streams(uint32_t nstates, uint32_t max_table_log, const uint8_t* d_in, uint64_t in_stride,
+                              const uint32_t* d_comp_len, uint32_t n_streams, uint8_t* d_out, uint32_t out_stride,
+                              uint32_t* d_out_len, int32_t* d_status, fsehip_stream_t stream) {
+    if (n_streams == 0) return FSE_ERR_EMPTY;
+    if (nstates > 2 || !d_in || !d_comp_len || !d_out || !d_out_len || !d_status || out_stride == 0 ||
+        (in_stride & 255u))
+        return FSE_ERR_BAD_ARG;
+    if (max_table_log > 15) return FSE_ERR_UNSUPPORTED;
+    const fsehip_params p{out_stride, 0, 0, max_table_log ? max_table_log : 11u, nstates ? nstates : 2u};
+    return with_dtables_n(&p, d_in, in_stride, d_comp_len, n_streams, stream,
+                          [&](const uint32_t* dt, const int32_t* info) {
+                              fsehip::DecParams P{};
+                              P.nstates = p.nstates;
+                              P.in = d_in;
+                              P.slot_bytes = in_stride;
+                              P.comp_len = d_comp_len;
+                              P.out = d_out;
+                              P.n_total = 0;  // reference mode: each stream ends where the crate's decoder stops
+                              P.block_size = out_stride;
+                              P.n_blocks = n_streams;
+                              P.out_cap = out_stride;
+                              P.status = d_status;
+                              P.out_len = d_out_len;
+                              P.dt = dt;
+                              P.dtinfo = info;
+                              return fsehip::launch_decode(P, kern_lmax(p.max_table_log),
+                                                           static_cast<hipStream_t>(stream)) == hipSuccess
+                                         ? (int)FSE_OK
+                                         : (int)FSE_ERR_HIP;
+                          });
 }
 
 int fsehip_histogram_blocks(const uint8_t* d_src, uint64_t n_total, uint32_t block_size, uint32_t* d_counts,

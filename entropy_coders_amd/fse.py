@@ -82,6 +82,37 @@ def decompress(src, cap: int = 1 << 24) -> bytes:
     return dst[: n.value].tobytes()
 
 
+def decompress_streams(streams, out_stride: int, nstates: int = 2, max_table_log: int = 11, device=None):
+    """`fsehip_decompress_streams`: many crate streams (no sidecar, no raw
+    length) decoded at once on the GPU, each as `fse_decompress2` (nstates 2)
+    or `fse_decompress` (1) would, within out_stride bytes.  Returns a list
+    with, per stream, its bytes or the name of its status."""
+    import torch
+
+    from ._lib import STATUS
+
+    dev = torch.device(device or "cuda")
+    stride = max(512, (max((len(x) for x in streams), default=1) + 255) // 256 * 256)
+    host = np.zeros(len(streams) * stride, dtype=np.uint8)
+    for i, x in enumerate(streams):
+        host[i * stride: i * stride + len(x)] = np.frombuffer(bytes(x), dtype=np.uint8)
+    d_in = torch.from_numpy(host).to(dev)
+    lens = torch.tensor([len(x) for x in streams], dtype=torch.int32, device=dev)
+    out = torch.empty(len(streams) * out_stride, dtype=torch.uint8, device=dev)
+    out_len = torch.zeros(len(streams), dtype=torch.int32, device=dev)
+    status = torch.zeros(len(streams), dtype=torch.int32, device=dev)
+    check(load().fsehip_decompress_streams(nstates, max_table_log, C.c_void_p(d_in.data_ptr()), stride,
+                                           C.c_void_p(lens.data_ptr()), len(streams), C.c_void_p(out.data_ptr()),
+                                           out_stride, C.c_void_p(out_len.data_ptr()),
+                                           C.c_void_p(status.data_ptr()),
+                                           C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)),
+          "fsehip_decompress_streams")
+    torch.cuda.synchronize(dev)
+    host_out, ol, st = out.cpu().numpy(), out_len.cpu().numpy(), status.cpu().numpy()
+    return [host_out[i * out_stride: i * out_stride + int(ol[i])].tobytes() if st[i] == 0 else
+            STATUS.get(int(st[i]), str(int(st[i]))) for i in range(len(streams))]
+
+
 def histogram_count(src) -> tuple[np.ndarray, int]:
     """`Histogram::new(data)` (histogram.rs:18-66): (counts[256], table_len)."""
     a = _buf(src)
@@ -359,6 +390,7 @@ class BlockCodec:
 
 __all__ = ["BITS_ADVANCE", "BITS_PEEK", "BITS_READ", "BlockCodec", "DecodeTable", "EncodeTable", "FseError",
            "Histogram", "NormHistogram", "bitstack_read", "bitstack_write", "bitstream_read", "compress", "compress2",
-           "compress2_log", "compress_nh", "decode_table_new", "decompress", "decompress2", "encode_table_new",
+           "compress2_log", "compress_nh", "decode_table_new", "decompress", "decompress2", "decompress_streams",
+           "encode_table_new",
            "histogram_count", "histogram_new", "norm_histogram_new", "norm_histogram_read", "norm_histogram_write",
            "normalize", "normalize_optimal"]

@@ -239,6 +239,20 @@ int fsehip_build_sidecar(const fsehip_params* p, const uint8_t* d_in, uint64_t s
 /* Compact the slot layout into one stream (blocks back to back at the byte
  * offsets d_offsets[b], an exclusive scan of d_comp_len) and back.  Used to
  * ship compressed shards between GPUs (RCCL gather) or to the host. */
+/* Batched fse_decompress2 / fse_decompress (nstates 2 / 1) in the crate's
+ * own termination (lib.rs:215-248 / 187-211), for streams with no sidecar
+ * and no recorded raw length, e.g. many outputs of the CPU crate.  Stream b:
+ * d_comp_len[b] bytes at d_in + b * in_stride (in_stride a multiple of 256
+ * and at least the largest stream; d_in 16-byte aligned); its output at d_out + b *
+ * out_stride, at most out_stride bytes; d_out_len[b] = bytes decoded.
+ * d_status[b]: DST_TOO_SMALL when out_stride is short, SINGLE_SYMBOL for a
+ * stream the crate would decode forever, UNSUPPORTED for a table log above
+ * max_table_log (0 = 11; 15 accepts every stream, on slower kernels).
+ * Serial per stream, many streams at once. */
+int fsehip_decompress_streams(uint32_t nstates, uint32_t max_table_log, const uint8_t* d_in, uint64_t in_stride,
+                              const uint32_t* d_comp_len, uint32_t n_streams, uint8_t* d_out, uint32_t out_stride,
+                              uint32_t* d_out_len, int32_t* d_status, fsehip_stream_t stream);
+
 int fsehip_pack_blocks(const uint8_t* d_slots, uint64_t slot_bytes, const uint32_t* d_comp_len,
                        const uint64_t* d_offsets, uint32_t n_blocks, uint8_t* d_stream, fsehip_stream_t stream);
 int fsehip_unpack_blocks(const uint8_t* d_stream, const uint64_t* d_offsets, const uint32_t* d_comp_len,

@@ -118,3 +118,41 @@ def test_random_host_calls(torch_cuda, case):
         assert got == want and bits == wbits, (case, L)
         if len(set(s.tolist())) > 1:  # a single-symbol stream never ends in the reference
             assert dec(got) == s.tobytes(), (case, L)
+
+
+@pytest.mark.parametrize("nstates", [2, 1])
+def test_decompress_streams(torch_cuda, nstates):
+    """fsehip_decompress_streams: a batch of crate streams of random sizes (no
+    sidecar, no raw length), some damaged, some single-symbol, some above
+    the table-log limit, each decoded as the crate's fse_decompress2 /
+    fse_decompress (reference mode, the oracle) would within the stride."""
+    from entropy_coders_amd import decompress_streams
+
+    rng = np.random.default_rng(0x57AE + nstates)
+    streams, logs = [], []
+    for i in range(60):
+        s = _block(rng, int(rng.integers(2, 20000)))
+        L = int(rng.choice([0, 0, 0, 9, 12, 13])) if nstates == 2 else 0
+        try:
+            comp = O.compress2(s, L or None)[0] if nstates == 2 else O.compress(s)[0]
+        except O.OracleError:
+            continue
+        comp = bytearray(comp)
+        if i % 11 == 5:  # damage
+            comp[int(rng.integers(0, len(comp)))] ^= 0x5A
+        streams.append(bytes(comp))
+        logs.append((comp[0] & 15) + 5)
+    stride = 24000
+    ref_dec = O.decompress2 if nstates == 2 else O.decompress
+    for mtl in (11, 15):
+        got = decompress_streams(streams, stride, nstates=nstates, max_table_log=mtl)
+        for i, (x, g) in enumerate(zip(streams, got)):
+            if logs[i] > mtl and logs[i] <= 15:
+                assert g == "UNSUPPORTED", (i, mtl, g)
+                continue
+            try:
+                want = ref_dec(x, stride)
+            except O.OracleError as e:
+                assert g == e.code, (i, mtl, e.code, g)
+                continue
+            assert g == want, (i, mtl)
