@@ -36,10 +36,27 @@ for name, kind, prob, tl in cases:
         ok = bool(torch.equal(out, src)) and int(st.abs().max()) == 0
         res[use] = (t, ok)
         out.fill_(0)
+    # the same blocks as crate streams with no raw length (fsehip_decompress_streams)
+    import ctypes as C
+    nb = codec.n_blocks(n)
+    ol = torch.zeros(nb, dtype=torch.int32, device="cuda")
+    lib, hs = codec.lib, C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    args = (ns, codec.max_table_log, C.c_void_p(cb["out"].data_ptr()), codec.slot_bytes,
+            C.c_void_p(cb["comp_len"].data_ptr()), nb, C.c_void_p(out.data_ptr()), codec.block_size,
+            C.c_void_p(ol.data_ptr()), C.c_void_p(st.data_ptr()), hs)
+    lib.fsehip_decompress_streams(*args)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rc = lib.fsehip_decompress_streams(*args)
+    torch.cuda.synchronize()
+    t_str = time.perf_counter() - t0
+    str_ok = rc == 0 and bool(torch.equal(out, src)) and int(st.abs().max()) == 0
+    res["streams"] = (t_str, str_ok)
     o2, side2, st2 = codec.build_sidecar(cb)
     torch.cuda.synchronize()
     side_ok = bool(torch.equal(o2, src)) and int(st2.abs().max()) == 0 and bool(torch.equal(side2, cb["sidecar"]))
     ratio = int(cb["comp_len"].sum()) / n
     print(f"{name} ({ns}-state): ratio {ratio:.3f}  sidecar {res[True][0] * 1e3:.2f} ms ({n / res[True][0] / 2**30:.0f} GiB/s, "
           f"ok={res[True][1]})  no sidecar {res[False][0] * 1e3:.2f} ms ({n / res[False][0] / 2**30:.1f} GiB/s, "
-          f"ok={res[False][1]})  build_sidecar ok={side_ok}", flush=True)
+          f"ok={res[False][1]})  streams {n / res['streams'][0] / 2**30:.1f} GiB/s ok={res['streams'][1]}  "
+          f"build_sidecar ok={side_ok}", flush=True)
