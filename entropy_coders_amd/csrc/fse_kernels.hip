@@ -391,20 +391,20 @@ template <int LMAX, int T>
 struct EncSmem {
     static constexpr int BPW = 64 / T;
     static constexpr uint32_t SIZE = 1u << LMAX;
-    uint16_t st[BPW][SIZE];
+    // A block's stateTable and symbol transforms are built last in phase 1,
+    // so until then they hold its scratch: the sub-histograms (4 KiB) and the
+    // spread's occurrence owners (2^L bytes) live in st[b], the rank loop's
+    // peer masks (512 B) in tt[b]
+    static_assert(2u * SIZE >= HIST_WORDS * 4u, "sub-histograms fit the stateTable");
+    __attribute__((aligned(16))) uint16_t st[BPW][SIZE];
     uint2 tt[BPW][256];
     // phase-1 scratch (statistics, header, spread) and phase-2 scratch
-    // (trajectories, end states, merge list) share the same LDS: 13.4 KB per
-    // workgroup at L <= 11, so 12 workgroups fit a CU (the VGPR limit)
+    // (trajectories, end states, merge list) share the same LDS
     union {
         struct {
             union {
-                uint32_t hs[HIST_WORDS];  // sub-histograms (counts[] go to cnt[], free until the spread)
                 uint32_t hdrw[HDR_MAX / 4];  // NCount header, stored to the slot before the spread
-                struct {
-                    __attribute__((aligned(16))) uint8_t sym_at[SIZE];
-                    __attribute__((aligned(16))) uint8_t occ_sym[SIZE];
-                } sp;
+                __attribute__((aligned(16))) uint8_t sym_at[SIZE];
             } u;
             int32_t norm[256];
             uint16_t cumul[256];
@@ -445,7 +445,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
         const uint32_t n = (uint32_t)min((uint64_t)P.block_size, P.n_total - off);
         const uint8_t* blk = P.src + off;
         uint32_t* counts = sm.ph.p1.cnt;  // the spread reuses cnt[] after normalize
-        const uint32_t tl = wave_histogram(blk, n, sm.ph.p1.u.hs, counts);
+        const uint32_t tl = wave_histogram(blk, n, reinterpret_cast<uint32_t*>(sm.st[b]), counts);
         FSE_STAMP(P, 1);
         if (P.debug & 8u) {  // ablation: histogram only
             if (lane == 0) P.status[gb] = (int32_t)tl;
@@ -479,11 +479,12 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
             const uint32_t size = 1u << L;
             uint16_t* st = sm.st[b];
             const uint16_t* cumul = sm.ph.p1.cumul;
-            rc = wave_build_spread(sm.ph.p1.norm, L, tl, sm.ph.p1.u.sp.sym_at, sm.ph.p1.u.sp.occ_sym, sm.ph.p1.cumul, sm.ph.p1.cnt,
+            rc = wave_build_spread(sm.ph.p1.norm, L, tl, sm.ph.p1.u.sym_at, reinterpret_cast<uint8_t*>(st), sm.ph.p1.cumul,
+                                   sm.ph.p1.cnt,
                                    [&](uint32_t i, uint32_t s, uint32_t r) {
                                        st[cumul[s] + r] = (uint16_t)(size + i);  // fse.rs:157-162
                                    },
-                                   nullptr, reinterpret_cast<uint64_t*>(sm.ph.p1.u.sp.occ_sym));
+                                   nullptr, reinterpret_cast<uint64_t*>(&sm.tt[b][0]));
             // symbol transforms, fse.rs:165-188 (total == cumul[s]), with
             // the stateTable's LDS address folded into deltaFindState
             const uint32_t stb = lds_addr_of(&sm.st[b][0]);
