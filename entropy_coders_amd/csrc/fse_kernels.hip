@@ -873,13 +873,24 @@ hipError_t launch_encode(const EncParams& P, uint32_t lmax, hipStream_t stream) 
     const uint32_t T = (P.lanes == 32 && lmax <= 12) ? 32u : 64u;
     const uint32_t bpw = 64u / T;
     const dim3 g((P.n_blocks + bpw - 1u) / bpw), b(64);
-    auto go = [&](auto kern) { hipLaunchKernelGGL(kern, g, b, P.xlds, stream, P); };
+    auto go = [&](auto kern, uint32_t pad = 0) { hipLaunchKernelGGL(kern, g, b, P.xlds ? P.xlds : pad, stream, P); };
     if (P.nstates == 1) {  // fse_compress (lib.rs:112-143)
         if (lmax <= 11) go(encode_blocks_kernel<11, 64, 1>);
         else if (lmax <= 12) go(encode_blocks_kernel<12, 64, 1>);
         else go(encode_blocks_kernel<15, 64, 1>);
     } else if (T == 64) {
-        if (lmax <= 11) go(encode_blocks_kernel<11, 64, 2>);
+        // 11 workgroups per CU rather than the 12 its 12.6 KB allow: same
+        // time on C2, 5% less on near-uniform data (tools/occ_enc.py, one
+        // process: 12 -> 2.00 ms, 11 -> 1.90, 10 -> 1.88; C2 1.58 / 1.57 /
+        // 1.61), where the twelfth workgroup only adds contention
+        static const uint32_t pad11 = [] {
+            hipFuncAttributes fa{};
+            if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(encode_blocks_kernel<11, 64, 2>)) != hipSuccess)
+                return 0u;
+            const size_t per = (160u << 10) / 11u - 64u;  // LDS per workgroup for 11, less allocation slack
+            return fa.sharedSizeBytes < per ? (uint32_t)(per - fa.sharedSizeBytes) : 0u;
+        }();
+        if (lmax <= 11) go(encode_blocks_kernel<11, 64, 2>, pad11);
         else if (lmax <= 12) go(encode_blocks_kernel<12, 64, 2>);
         else go(encode_blocks_kernel<15, 64, 2>);
     } else {
