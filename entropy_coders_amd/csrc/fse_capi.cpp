@@ -379,6 +379,7 @@ int fsehip_build_dtables(const fsehip_params* p, const uint8_t* d_in, uint64_t s
     D.n_blocks = n_blocks;
     D.dt = d_dtables;
     D.dtinfo = d_dtinfo;
+    D.xlds = env_u32("FSEHIP_DT_XLDS", 0);  // diagnostics: occupancy probe
     hipError_t e = fsehip::launch_dtables(D, kern_lmax(p->max_table_log), static_cast<hipStream_t>(stream));
     return e == hipSuccess ? FSE_OK : FSE_ERR_HIP;
 }

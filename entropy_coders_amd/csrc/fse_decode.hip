@@ -1222,9 +1222,9 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
 
 hipError_t launch_dtables(const DtParams& P, uint32_t lmax, hipStream_t stream) {
     const dim3 g(P.n_blocks), b(64);
-    if (lmax <= 11) hipLaunchKernelGGL((dtable_blocks_kernel<11>), g, b, 0, stream, P);
-    else if (lmax <= 12) hipLaunchKernelGGL((dtable_blocks_kernel<12>), g, b, 0, stream, P);
-    else hipLaunchKernelGGL((dtable_blocks_kernel<15>), g, b, 0, stream, P);
+    if (lmax <= 11) hipLaunchKernelGGL((dtable_blocks_kernel<11>), g, b, P.xlds, stream, P);
+    else if (lmax <= 12) hipLaunchKernelGGL((dtable_blocks_kernel<12>), g, b, P.xlds, stream, P);
+    else hipLaunchKernelGGL((dtable_blocks_kernel<15>), g, b, P.xlds, stream, P);
     return hipGetLastError();
 }
 

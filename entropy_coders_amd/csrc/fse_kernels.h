@@ -61,6 +61,7 @@ struct DtParams {
     uint32_t n_blocks;
     uint32_t* dt;      // [n_blocks][1 << lmax] entries (dte_make layout)
     int32_t* dtinfo;   // header bytes | L << 16, or < 0 = status
+    uint32_t xlds;     // diagnostics: extra dynamic LDS bytes per workgroup (occupancy probe)
 };
 
 struct GenParams {
