@@ -452,8 +452,10 @@ def compress2(src: bytes, log2: int | None = None) -> tuple[bytes, int]:
     return head + sink.to_bytes(), len(sink.bits)
 
 
-def compress(src: bytes) -> tuple[bytes, int]:
-    """fse_compress, one state (lib.rs:112-143)."""
+def compress_headerless(src: bytes):
+    """The crate's test-module fse_compress (fse.rs:394-421): the 1-state
+    stream of lib.rs:112-143 with no header in front (the caller keeps the
+    NormHistogram).  Returns (norm, L, table_len, payload, payload bits)."""
     counts, size, tl = histogram(src)
     if size == 0:
         raise SpecError("EMPTY")
@@ -462,7 +464,6 @@ def compress(src: bytes) -> tuple[bytes, int]:
     if size == 1:
         raise SpecError("TOO_SHORT")
     norm, L, _ = normalize(counts, size, tl, optimal_log2(size, tl))
-    head = header_write(norm, L, tl)
     tab = encode_table(norm, L, tl)
     sink = BitSink()
     n = len(src)
@@ -476,7 +477,14 @@ def compress(src: bytes) -> tuple[bytes, int]:
         e.step(ch[0], sink)
     e.finish(L, sink)
     sink.put(1, 1)
-    return head + sink.to_bytes(), len(sink.bits)
+    return norm, L, tl, sink.to_bytes(), len(sink.bits)
+
+
+def compress(src: bytes) -> tuple[bytes, int]:
+    """fse_compress, one state (lib.rs:112-143): the header (hist.write) and,
+    from the next byte on, the headerless stream."""
+    norm, L, tl, payload, bits = compress_headerless(src)
+    return header_write(norm, L, tl) + payload, bits
 
 
 def _single_symbol(norm, L) -> bool:
@@ -525,10 +533,10 @@ def decompress2(data: bytes, raw_len: int | None = None) -> bytes:
     return bytes(out)
 
 
-def decompress(data: bytes) -> bytes:
-    """fse_decompress, one state (lib.rs:187-211)."""
-    norm, L, tl, used = header_read(data)
-    stack = Stack(data[used:])
+def decompress_headerless(norm, L, tl, payload: bytes) -> bytes:
+    """The crate's test-module fse_decompress (fse.rs:424-434): the table from
+    the caller's NormHistogram, then the lib.rs:187-211 loop."""
+    stack = Stack(payload)
     dt = decode_table(norm, L, tl)
     if _single_symbol(norm, L):
         raise SpecError("SINGLE_SYMBOL")
@@ -545,6 +553,12 @@ def decompress(data: bytes) -> bytes:
         out.append(sym)
     out.append(dt[st][1])
     return bytes(out)
+
+
+def decompress(data: bytes) -> bytes:
+    """fse_decompress, one state (lib.rs:187-211)."""
+    norm, L, tl, used = header_read(data)
+    return decompress_headerless(norm, L, tl, data[used:])
 
 
 # ---------------------------------------------------------------- generators

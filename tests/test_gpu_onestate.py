@@ -177,3 +177,20 @@ def test_batched_onestate_prebuilt_tables(torch_cuda):
         assert int(st.abs().max()) == 0
         src = codec.generate(2, 0.0, 0x5EED1001, cb["n_total"])
         assert torch.equal(out, src)
+
+
+def test_headerless_variant(torch_cuda):
+    """The crate's test-module 1-state codec (fse.rs:394-434) writes the
+    fse_compress stream without a header: the GPU fse_compress bytes after the
+    header are exactly that stream, and a headerless stream decodes once its
+    NormHistogram is written in front of it (norm_histogram_write)."""
+    from oracle import spec as S
+    from entropy_coders_amd import compress_nh, decompress, norm_histogram_write
+
+    for prob, n in ((0.2, 1 << 15), (0.5, 333), (0.05, 4096)):
+        src = O.generate(0, prob, 0x5EED0001, 0, n).tobytes()
+        norm, L, tl, payload, bits = S.compress_headerless(src)
+        comp, cbits, nh = compress_nh(src)
+        head, _ = norm_histogram_write(nh)
+        assert comp == head + payload and cbits == bits
+        assert decompress(head + payload) == src

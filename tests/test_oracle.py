@@ -254,3 +254,16 @@ def test_oracle_matches_spec_random(case):
         assert got == want, case
         if len(set(src)) > 1:
             assert dec_s(want[0]) == src, case
+
+
+@pytest.mark.parametrize("prob,n", [(0.2, 1 << 15), (0.5, 333), (0.05, 4096), (0.77, 1001)])
+def test_headerless_variant(prob, n):
+    """fse.rs:394-434 (the crate's own compress / decompress tests): the
+    headerless 1-state stream is lib.rs's fse_compress output after its
+    header, and decodes back with the caller's NormHistogram."""
+    src = O.generate(0, prob, 0x5EED0001, 0, n).tobytes()
+    norm, L, tl, payload, bits = S.compress_headerless(src)
+    whole, wbits = O.compress(src)
+    head = S.header_write(norm, L, tl)
+    assert whole == head + payload and wbits == bits
+    assert S.decompress_headerless(norm, L, tl, payload) == src
