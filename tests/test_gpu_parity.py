@@ -150,3 +150,17 @@ def test_batched_1gib_digest(torch_cuda):
     cb = _batched_roundtrip(torch, 0, 0.155, 0, 1 << 30, check_all=False)
     ratio = float(cb["comp_len"].double().sum()) / (1 << 30)
     assert 0.49 < ratio < 0.52
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_reference_lib_tests(torch_cuda, seed):
+    """lib.rs:280-302 (the crate's compress / compress2 tests): LUT p=0.2
+    sequences of 2^16 bytes round-trip through fse_compress / fse_decompress
+    and fse_compress2 / fse_decompress2, and the bytes equal the oracle's."""
+    from entropy_coders_amd import compress, compress2, decompress, decompress2
+
+    src = O.generate(0, 0.2, 0x11B0 + seed, 0, 1 << 16)
+    for enc, dec, ref in ((compress, decompress, O.compress), (compress2, decompress2, O.compress2)):
+        comp, bits = enc(src)
+        assert (comp, bits) == ref(src)
+        assert dec(comp) == src.tobytes()
