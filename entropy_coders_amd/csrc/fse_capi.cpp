@@ -452,7 +452,7 @@ int fsehip_decompress_streams(uint32_t nstates, uint32_t max_table_log, const ui
                               uint32_t* d_out_len, int32_t* d_status, fsehip_stream_t stream) {
     if (n_streams == 0) return FSE_ERR_EMPTY;
     if (nstates > 2 || !d_in || !d_comp_len || !d_out || !d_out_len || !d_status || out_stride == 0 ||
-        (in_stride & 255u))
+        (in_stride & 255u) || (reinterpret_cast<uintptr_t>(d_in) & 15u))
         return FSE_ERR_BAD_ARG;
     if (max_table_log > 15) return FSE_ERR_UNSUPPORTED;
     const fsehip_params p{out_stride, 0, 0, max_table_log ? max_table_log : 11u, nstates ? nstates : 2u};

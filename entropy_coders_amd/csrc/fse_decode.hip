@@ -512,6 +512,7 @@ __global__ __launch_bounds__(64) void dtable_blocks_kernel(DtParams P) {
     const int hl = header_read_wave(r0, r1, clen, (uint32_t)LMAX, norm, &L, &tl);
     int rc = hl < 0 ? hl : FSE_OK;
     if (rc == FSE_OK && ((uint32_t)hl >= clen || last == 0)) rc = FSE_ERR_NO_MARKER;  // lib.rs:222
+    if (rc == FSE_OK && clen > (1u << 28)) rc = FSE_ERR_UNSUPPORTED;  // bit positions are 32-bit in the decoders
     wave_sync();
     if (rc == FSE_OK) {
         const uint32_t size = 1u << L;

@@ -247,7 +247,8 @@ int fsehip_build_sidecar(const fsehip_params* p, const uint8_t* d_in, uint64_t s
  * out_stride, at most out_stride bytes; d_out_len[b] = bytes decoded.
  * d_status[b]: DST_TOO_SMALL when out_stride is short, SINGLE_SYMBOL for a
  * stream the crate would decode forever, UNSUPPORTED for a table log above
- * max_table_log (0 = 11; 15 accepts every stream, on slower kernels).
+ * max_table_log (0 = 11; 15 accepts every stream, on slower kernels) or a
+ * stream above 2^28 bytes.
  * Serial per stream, many streams at once. */
 int fsehip_decompress_streams(uint32_t nstates, uint32_t max_table_log, const uint8_t* d_in, uint64_t in_stride,
                               const uint32_t* d_comp_len, uint32_t n_streams, uint8_t* d_out, uint32_t out_stride,
