@@ -781,18 +781,20 @@ __global__ __launch_bounds__(64) void serial2_decode_kernel(DecParams P) {
 // prefetched registers at each refill branch, so it waits for the load,
 // and for any output store issued after it).  Here:
 //   - K blocks per workgroup, lane j of wave 0 walking block j: one VALU
-//     instruction advances K chains (K = 4 at L <= 11: 4 x (8 KiB table +
-//     1 KiB ring) = 36 KB, 4 workgroups = 16 chains per CU);
-//   - wave 1 streams each block's payload top down into its 256-word LDS
-//     ring in 256-byte chunks (one dword per lane), as far ahead as the ring
-//     allows, and publishes the lowest word landed (ctl[0]);
+//     instruction advances K chains, and LDS caps the chains per CU (K = 6
+//     at L <= 11: 6 x (6 KiB table + 512 B ring) = 40.0 KB, 4 workgroups =
+//     24 chains per CU; K = 3 at L = 12: 3 x 12.5 KiB, 12 chains per CU);
+//   - wave 1 streams each block's payload top down into its 128-word LDS
+//     ring in 256-byte chunks (one dword per lane), one chunk ahead of the
+//     one being decoded (a chunk lasts ~170 pairs, ~17 us: far longer than a
+//     load), and publishes the lowest word landed (ctl[0]);
 //   - the decode lanes read only LDS (one payload word and the two table
 //     entries per pair, issued together, as the segment decoder's
 //     LdsChain), publish the highest word they may still read every 8 pairs
 //     (ctl[1]) and store their output without ever waiting on memory.
 // Same end checks, statuses and sidecar recording as serial2.
 // ------------------------------------------------------------------------
-constexpr uint32_t RING_WORDS = 256u, RING_MASK = RING_WORDS - 1u, RING_CHUNK = 64u;
+constexpr uint32_t RING_WORDS = 128u, RING_MASK = RING_WORDS - 1u, RING_CHUNK = 64u;
 
 // Relaxed workgroup-scope atomics keep these as plain ds_read/ds_write (a
 // volatile access through a generic pointer becomes a FLAT access that
@@ -820,30 +822,31 @@ __device__ __forceinline__ void lds_store_release(int32_t* p, int32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// The sidecar-less decoder's table in LDS, per block.  L <= 11 (COMPACT):
-// u16 entries nb | newState << 5 plus a u8 symbol array, 6 KiB instead of
-// 8 KiB, so 5 blocks fit a workgroup where 4 did; L = 12: the u32 entries of
-// dtable_blocks_kernel (nb | sym << 8 | newState << 18).  Either way the low
-// five bits are nb (nb <= 15, the next field starts at bit 5 or 8), so
-// v_bfe can take the entries themselves as width / offset operands, and
-// e >> SH is the byte offset of entry newState.
-template <bool COMPACT>
+// The sidecar-less decoder's table in LDS, per block: u16 entries
+// nb | newState << NBW plus a u8 symbol array, 3 bytes per state (6 KiB at
+// L = 11, 12 KiB at L = 12, against 8 / 16 KiB of dtable_blocks_kernel's u32
+// entries), so 5 blocks fit a workgroup at L <= 11 and 3 at L = 12.
+// NBW = 5 (L <= 11): nb < 16 leaves bit 4 clear, so v_bfe takes the entries
+// themselves as width / offset operands and e >> 4 is the byte offset of
+// entry newState.  NBW = 4 (L = 12, newState needs 12 bits): nb is masked
+// out (e & 15) and the offset is (e >> 3) & ~1.
+template <uint32_t NBW>
 struct RingTab {
-    static constexpr uint32_t SH = COMPACT ? 4u : 16u;  // e >> SH = newState * entry bytes
-    static constexpr uint32_t ESH = COMPACT ? 1u : 2u;  // log2 entry bytes
-    const uint8_t* ent;                                 // entries
-    const uint8_t* sym;                                 // COMPACT: symbols
+    static_assert(NBW == 4 || NBW == 5, "nb field width");
+    const uint8_t* ent;  // entries
+    const uint8_t* sym;  // symbols
     __device__ __forceinline__ uint32_t entry_at(uint32_t a) const {  // a = byte offset
-        return COMPACT ? (uint32_t)*reinterpret_cast<const uint16_t*>(ent + a)
-                       : *reinterpret_cast<const uint32_t*>(ent + a);
+        return (uint32_t)*reinterpret_cast<const uint16_t*>(ent + a);
     }
-    __device__ __forceinline__ uint32_t sym_at(uint32_t a, uint32_t e) const {
-        return COMPACT ? (uint32_t)sym[a >> 1] : (e >> 8) & 0xFFu;
-    }
+    __device__ __forceinline__ uint32_t sym_at(uint32_t a) const { return (uint32_t)sym[a >> 1]; }
+    // nb as a bit-field operand (v_bfe reads its low five bits)
+    __device__ __forceinline__ uint32_t nbf(uint32_t e) const { return NBW == 5 ? e : e & 15u; }
+    // byte offset of entry newState
+    __device__ __forceinline__ uint32_t base(uint32_t e) const { return NBW == 5 ? e >> 4 : (e >> 3) & ~1u; }
     // by state index (end-of-block steps)
-    __device__ __forceinline__ uint32_t nb(uint32_t s) const { return entry_at(s << ESH) & 31u; }
-    __device__ __forceinline__ uint32_t symbol(uint32_t s) const { return sym_at(s << ESH, entry_at(s << ESH)); }
-    __device__ __forceinline__ uint32_t next_base(uint32_t s) const { return (entry_at(s << ESH) >> SH) >> ESH; }
+    __device__ __forceinline__ uint32_t nb(uint32_t s) const { return entry_at(s << 1) & ((1u << NBW) - 1u); }
+    __device__ __forceinline__ uint32_t symbol(uint32_t s) const { return (uint32_t)sym[s]; }
+    __device__ __forceinline__ uint32_t next_base(uint32_t s) const { return base(entry_at(s << 1)) >> 1; }
 };
 
 // LdsChain over the ring.  NS = 2: a pair (<= 24 bits) per step; NS = 1:
@@ -851,39 +854,40 @@ struct RingTab {
 // and lo moves down by at most one word per step, so the upper word is
 // either the previous upper word or the previous lower one.  a0 / a1 are
 // the states' entry byte offsets.
-template <int NS, bool COMPACT>
+template <int NS, uint32_t NBW>
 struct RingChain {
     static constexpr int32_t OFF = 12 * NS;
-    using Tab = RingTab<COMPACT>;
+    using Tab = RingTab<NBW>;
     int32_t pos, B;
     uint32_t whi, wlo, a0, a1;
     __device__ __forceinline__ void init(const uint32_t* ring, int32_t p, uint32_t s0, uint32_t s1) {
         pos = p;
-        a0 = s0 << Tab::ESH;
-        a1 = s1 << Tab::ESH;
+        a0 = s0 << 1;
+        a1 = s1 << 1;
         B = (p - OFF) & ~31;
         wlo = 0;
         whi = ring[((uint32_t)(B >> 5) + 1u) & RING_MASK];
     }
-    __device__ __forceinline__ uint32_t s0() const { return a0 >> Tab::ESH; }
-    __device__ __forceinline__ uint32_t s1() const { return a1 >> Tab::ESH; }
+    __device__ __forceinline__ uint32_t s0() const { return a0 >> 1; }
+    __device__ __forceinline__ uint32_t s1() const { return a1 >> 1; }
     // one pair; returns sym0 | sym1 << 8
     __device__ __forceinline__ uint32_t pair(const uint32_t* ring, const Tab& T) {
         const int32_t lo = (pos - OFF) & ~31;
         const uint32_t w0 = ring[(uint32_t)(lo >> 5) & RING_MASK];
         const uint32_t e0 = T.entry_at(a0);
         const uint32_t e1 = T.entry_at(a1);
-        const uint32_t y0 = T.sym_at(a0, e0), y1 = T.sym_at(a1, e1);
+        const uint32_t y0 = T.sym_at(a0), y1 = T.sym_at(a1);
         const uint32_t w1 = lo == B ? whi : wlo;
-        pos -= (int32_t)((e0 + e1) & 31u);
+        const uint32_t n0 = T.nbf(e0), n1 = T.nbf(e1);
+        pos -= (int32_t)((n0 + n1) & 31u);
         const uint32_t x = (uint32_t)((((uint64_t)w1 << 32) | w0) >> (uint32_t)(pos - lo));
         B = lo;
         whi = w1;
         wlo = w0;
-        const uint32_t v1 = __builtin_amdgcn_ubfe(x, 0u, e1);
-        const uint32_t v0 = __builtin_amdgcn_ubfe(x, e1, e0);
-        a0 = (e0 >> Tab::SH) + (v0 << Tab::ESH);
-        a1 = (e1 >> Tab::SH) + (v1 << Tab::ESH);
+        const uint32_t v1 = __builtin_amdgcn_ubfe(x, 0u, n1);
+        const uint32_t v0 = __builtin_amdgcn_ubfe(x, n1, n0);
+        a0 = T.base(e0) + (v0 << 1);
+        a1 = T.base(e1) + (v1 << 1);
         return y0 | (y1 << 8);
     }
     // NS = 1: one symbol; returns it
@@ -891,14 +895,15 @@ struct RingChain {
         const int32_t lo = (pos - OFF) & ~31;
         const uint32_t w0 = ring[(uint32_t)(lo >> 5) & RING_MASK];
         const uint32_t e = T.entry_at(a0);
-        const uint32_t y = T.sym_at(a0, e);
+        const uint32_t y = T.sym_at(a0);
         const uint32_t w1 = lo == B ? whi : wlo;
-        pos -= (int32_t)(e & 31u);
+        const uint32_t n0 = T.nbf(e);
+        pos -= (int32_t)(n0 & 31u);
         const uint32_t x = (uint32_t)((((uint64_t)w1 << 32) | w0) >> (uint32_t)(pos - lo));
         B = lo;
         whi = w1;
         wlo = w0;
-        a0 = (e >> Tab::SH) + (__builtin_amdgcn_ubfe(x, 0u, e) << Tab::ESH);
+        a0 = T.base(e) + (__builtin_amdgcn_ubfe(x, 0u, n0) << 1);
         return y;
     }
 };
@@ -907,9 +912,9 @@ template <int LMAX, uint32_t K, int NS>
 __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
     static_assert(LMAX <= 12, "entry layout ns << 18: e >> 16 is the next entry's byte offset");
     static_assert(K >= 1 && K <= 64, "one decode lane per block");
-    constexpr bool COMPACT = LMAX <= 11;  // newState < 2^11: nb | ns << 5 fits 16 bits
+    constexpr uint32_t NBW = LMAX <= 11 ? 5u : 4u;  // nb | newState << NBW fits 16 bits
     constexpr uint32_t TW = 1u << LMAX;
-    constexpr uint32_t TAB_BYTES = COMPACT ? 3u * TW : 4u * TW;  // per block
+    constexpr uint32_t TAB_BYTES = 3u * TW;  // per block: u16 entries + u8 symbols
     __shared__ __attribute__((aligned(16))) uint8_t tab_all[K * TAB_BYTES];
     __shared__ uint32_t ring_all[K * RING_WORDS];
     __shared__ int32_t ctl_all[K][2];  // [0] lowest word landed, [1] highest word the decoder may still read; INT32_MIN = stop
@@ -936,16 +941,14 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
         uint32_t nbor = 0;
         for (uint32_t i = tid; i < nv; i += 128u) {
             const uint4 q = t4[i];
-            if (COMPACT) {  // nb | ns << 5 (ns = e >> 18) and the symbols, 4 entries at a time
-                auto c16 = [](uint32_t e) { return (e & 0xFu) | ((e >> 13) & ~31u); };
-                reinterpret_cast<uint2*>(tb)[i] =
-                    make_uint2(c16(q.x) | (c16(q.y) << 16), c16(q.z) | (c16(q.w) << 16));
-                reinterpret_cast<uint32_t*>(tb + 2u * TW)[i] =
-                    __builtin_amdgcn_perm(__builtin_amdgcn_perm(q.w, q.z, 0x0c0c0501u),
-                                          __builtin_amdgcn_perm(q.y, q.x, 0x0c0c0501u), 0x05040100u);
-            } else {
-                reinterpret_cast<uint4*>(tb)[i] = q;
-            }
+            // nb | ns << NBW (ns = e >> 18; bits 16, 17 of e are clear) and the
+            // symbols, 4 entries at a time
+            auto c16 = [](uint32_t e) { return (e & 0xFu) | ((e >> (18u - NBW)) & ~((1u << NBW) - 1u)); };
+            reinterpret_cast<uint2*>(tb)[i] =
+                make_uint2(c16(q.x) | (c16(q.y) << 16), c16(q.z) | (c16(q.w) << 16));
+            reinterpret_cast<uint32_t*>(tb + 2u * TW)[i] =
+                __builtin_amdgcn_perm(__builtin_amdgcn_perm(q.w, q.z, 0x0c0c0501u),
+                                      __builtin_amdgcn_perm(q.y, q.x, 0x0c0c0501u), 0x05040100u);
             nbor |= (q.x | q.y | q.z | q.w) & 0xFFu;
         }
         if (nbor) atomicOr(&any_nb[j], 1u);
@@ -1003,7 +1006,7 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
     if (lane >= K || gb >= P.n_blocks) return;
 
     // wave 0, lane j < K: the decoder of block gb0 + j
-    const RingTab<COMPACT> T{tab_all + lane * TAB_BYTES, tab_all + lane * TAB_BYTES + 2u * TW};
+    const RingTab<NBW> T{tab_all + lane * TAB_BYTES, tab_all + lane * TAB_BYTES + 2u * TW};
     const uint32_t* const ring = ring_all + lane * RING_WORDS;
     int32_t* const ctl = ctl_all[lane];
     const int32_t info = P.dtinfo[gb];
@@ -1046,7 +1049,7 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
         wait_words((top - NS * (int32_t)L) >> 5);
         const uint32_t s0i = bits_at(top - (int32_t)L) & ((1u << L) - 1u);
         const uint32_t s1i = NS == 2 ? bits_at(top - 2 * (int32_t)L) & ((1u << L) - 1u) : 0u;
-        RingChain<NS, COMPACT> c;
+        RingChain<NS, NBW> c;
         c.init(ring, top - NS * (int32_t)L, s0i, s1i);
         const uint32_t I = P.ckpt_interval;
         uint64_t* rec = (P.sidecar_out && I) ? P.sidecar_out + gb * P.ckpt_per_block : nullptr;
@@ -1184,13 +1187,13 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
     if (!P.dt || !P.dtinfo) return hipErrorInvalidValue;
     if (!P.sidecar) {  // serial: sidecar-less blocks, reference-mode host streams, sidecar recording
         if (P.nstates == 1) {
-            if (lmax <= 11) hipLaunchKernelGGL((serial_ring_kernel<11, 5, 1>), dim3((P.n_blocks + 4u) / 5u), dim3(128), 0, stream, P);
-            else if (lmax <= 12) hipLaunchKernelGGL((serial_ring_kernel<12, 2, 1>), dim3((P.n_blocks + 1u) / 2u), dim3(128), 0, stream, P);
+            if (lmax <= 11) hipLaunchKernelGGL((serial_ring_kernel<11, 6, 1>), dim3((P.n_blocks + 5u) / 6u), dim3(128), 0, stream, P);
+            else if (lmax <= 12) hipLaunchKernelGGL((serial_ring_kernel<12, 3, 1>), dim3((P.n_blocks + 2u) / 3u), dim3(128), 0, stream, P);
             else hipLaunchKernelGGL((decode1_serial_kernel<15>), g, dim3(64), 0, stream, P);
         } else {
-            // 5 (L <= 11, compact tables) or 2 (L = 12) blocks per workgroup: 20 / 8 chains per CU (LDS-bound)
-            if (lmax <= 11) hipLaunchKernelGGL((serial_ring_kernel<11, 5, 2>), dim3((P.n_blocks + 4u) / 5u), dim3(128), 0, stream, P);
-            else if (lmax <= 12) hipLaunchKernelGGL((serial_ring_kernel<12, 2, 2>), dim3((P.n_blocks + 1u) / 2u), dim3(128), 0, stream, P);
+            // 6 (L <= 11) or 3 (L = 12) blocks per workgroup: 24 / 12 chains per CU (LDS-bound)
+            if (lmax <= 11) hipLaunchKernelGGL((serial_ring_kernel<11, 6, 2>), dim3((P.n_blocks + 5u) / 6u), dim3(128), 0, stream, P);
+            else if (lmax <= 12) hipLaunchKernelGGL((serial_ring_kernel<12, 3, 2>), dim3((P.n_blocks + 2u) / 3u), dim3(128), 0, stream, P);
             else hipLaunchKernelGGL((serial2_decode_kernel<15>), g, dim3(64), 0, stream, P);
         }
         return hipGetLastError();
