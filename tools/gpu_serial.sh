@@ -1,3 +1,5 @@
+# Sidecar-less decode check: the whole -m gpu suite, then tools/nosidecar_time.py
+# (2-state and 1-state at 256 MiB, C2 and skewed L=12 at 1 GiB).
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 900 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > gpurun_out/t_all.log 2>&1 && tail -3 gpurun_out/t_all.log &&
