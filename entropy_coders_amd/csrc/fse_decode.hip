@@ -825,7 +825,8 @@ __device__ __forceinline__ void lds_store_release(int32_t* p, int32_t v) {
 // The sidecar-less decoder's table in LDS, per block: u16 entries
 // nb | newState << NBW plus a u8 symbol array, 3 bytes per state (6 KiB at
 // L = 11, 12 KiB at L = 12, against 8 / 16 KiB of dtable_blocks_kernel's u32
-// entries), so 5 blocks fit a workgroup at L <= 11 and 3 at L = 12.
+// entries), so with 512-byte rings 6 blocks fit a 40 KB workgroup at
+// L <= 11 and 3 at L = 12 (4 workgroups per CU).
 // NBW = 5 (L <= 11): nb < 16 leaves bit 4 clear, so v_bfe takes the entries
 // themselves as width / offset operands and e >> 4 is the byte offset of
 // entry newState.  NBW = 4 (L = 12, newState needs 12 bits): nb is masked
