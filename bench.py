@@ -110,7 +110,8 @@ def host_cpu() -> dict:
                     break
     except OSError:
         pass
-    return {"nproc": n_aff, "cgroup_cpu_quota": quota, "model": model}
+    usable = n_aff if quota is None else max(1, min(n_aff, int(quota)))
+    return {"nproc": n_aff, "cgroup_cpu_quota": quota, "usable_cores": usable, "model": model}
 
 
 def workload_name(args, n: int) -> str:
@@ -143,10 +144,13 @@ def _median_rate(fn, nbytes: int, budget_s: float) -> float:
 def cpu_baseline(src_host: np.ndarray, block: int, budget_s: float) -> dict:
     """The parity oracle (C restatement of the reference, -O3) on host cores.
 
-    (ii) All host cores: whole 64 KiB blocks of the same C2 data,
-    compressed+decompressed by one pthread per core of this process's CPU
-    affinity (`nproc`); repeated over the first blocks until ~budget_s/2 of
-    wall time has been spent, throughput = raw bytes / wall time.
+    (ii) All usable host cores: whole 64 KiB blocks of the same C2 data,
+    compressed+decompressed by one pthread per usable core -- min(CPU
+    affinity, cgroup CPU quota), so threads never time-share a quota -- and
+    repeated over the first blocks until ~budget_s/2 of wall time has been
+    spent, throughput = raw bytes / wall time.  The same round trip on ONE
+    thread is timed beside it (`single_core_c2_GiB_s`) so the multi-core
+    figure can be checked against cores x single-core.
     (i) Single core, single block (benches/fse_benchmark.rs semantics): C1
     (64 KiB geometric p=0.5) and the bench-exact 32 KiB LUT p=0.2 block,
     median of repeated batches.
@@ -154,7 +158,7 @@ def cpu_baseline(src_host: np.ndarray, block: int, budget_s: float) -> dict:
     from oracle import oracle as O
 
     host = host_cpu()
-    threads = max(1, host["nproc"])
+    threads = host["usable_cores"]
     n_blocks = len(src_host) // block
     # calibrate on a small slice
     sample = src_host[: block * min(n_blocks, max(threads * 4, 64))]
@@ -177,6 +181,17 @@ def cpu_baseline(src_host: np.ndarray, block: int, budget_s: float) -> dict:
         total += len(sample)
         reps += 1
     assert np.array_equal(out, sample)
+    # the same C2 round trip on one thread (bounded: ~budget_s/8)
+    one = src_host[: block * min(n_blocks, 64)]
+    t_one, n_one = 0.0, 0
+    while t_one < budget_s / 8 or n_one == 0:
+        t0 = time.perf_counter()
+        c1, l1, s1 = O.compress2_blocks(one, block, 1)
+        o1 = O.decompress2_blocks(c1, s1, l1, block, len(one), 1)
+        t_one += time.perf_counter() - t0
+        n_one += len(one)
+    assert np.array_equal(o1, one)
+    single_c2 = n_one / t_one / 2**30
     single = {}
     for name, kind, prob, nb in (("C1_64KiB_geometric_p0.5", 1, 0.5, 1 << 16),
                                  ("bench_exact_32KiB_lut_p0.2", 0, 0.2, 1 << 15)):
@@ -193,16 +208,21 @@ def cpu_baseline(src_host: np.ndarray, block: int, budget_s: float) -> dict:
         "cores": threads,
         "kind": "port",
         "sample": f"{reps} x {n_take >> 20} MiB of the same C2 data ({n_take // block} x 64 KiB blocks), "
-                  f"compress2+decompress2 round trip, {threads} pthreads (one per core of the process's "
-                  f"CPU affinity), oracle/fse_oracle.c -O3",
+                  f"compress2+decompress2 round trip, {threads} pthreads (one per usable core: "
+                  f"min(affinity {host['nproc']}, cgroup quota {host['cgroup_cpu_quota']})), "
+                  f"oracle/fse_oracle.c -O3",
+        "single_core_c2_GiB_s": round(single_c2, 4),
+        "vs_cores_x_single": round(total / wall / 2**30 / (threads * single_c2), 3),
         "host": host,
         "single_core": single,
     }
 
 
+FSE_ERR_ENCODER_INIT = -17  # include/fse_status.h
+
 C5_SWEEP = [  # BASELINE.json configs[4]: (name, generator kind, LUT p, table log)
-    *[("near-uniform (0..239, H~7.9 bits)", 2, 0.0, L) for L in (9, 10, 11, 12)],
-    *[("skewed (LUT p=0.77, H~1.0 bit)", 0, 0.77, L) for L in (9, 10, 11, 12)],
+    *[("near-uniform (0..239, H~7.9 bits)", 2, 0.0, L) for L in (9, 10, 11, 12, 13, 14, 15)],
+    *[("skewed (LUT p=0.77, H~1.0 bit)", 0, 0.77, L) for L in (9, 10, 11, 12, 13, 14, 15)],
     ("LUT p=0.05 (normalize_slow path)", 0, 0.05, 9),
 ]
 
@@ -221,6 +241,15 @@ def c5_sweep(dev, nbytes: int, block: int, ckpt: int, reps: int = 3) -> list:
     for name, kind, prob, L in C5_SWEEP:
         codec = BlockCodec(block_size=block, table_log=L, ckpt_interval=ckpt, device=dev)
         src = codec.generate(kind, prob, 0x5EED0005, nbytes)
+        if L == 15:
+            # the crate's new_first_symbol panics at L = 15 unless both seed
+            # symbols (the block's last two bytes) have a power-of-two count
+            # (fse.rs:210-218): seed every block with two symbols outside
+            # the alphabet (count 1 -> norm -1), so the row times real blocks
+            full_b = nbytes // block
+            seeds = src[: full_b * block].view(full_b, block)
+            seeds[:, -2] = 250
+            seeds[:, -1] = 251
         cb = codec.alloc(nbytes)
         out = torch.empty(nbytes, dtype=torch.uint8, device=dev)
         st = torch.zeros(codec.n_blocks(nbytes), dtype=torch.int32, device=dev)
@@ -237,12 +266,34 @@ def c5_sweep(dev, nbytes: int, block: int, ckpt: int, reps: int = 3) -> list:
         torch.cuda.synchronize(dev)
         enc_ms = ev[0].elapsed_time(ev[1]) / reps
         dec_ms = ev[1].elapsed_time(ev[2]) / reps
-        ok = (int(cb["status"].abs().max()) == 0 and int(st.abs().max()) == 0 and bool(torch.equal(out, src)))
+        # At L = 15 the crate's Encoder::new_first_symbol (fse.rs:210-218)
+        # panics whenever a seed symbol's count is not a power of two (its
+        # wrapped u32 index leaves the table): those blocks report
+        # ENCODER_INIT, as the reference would panic on them.  Every other
+        # block must encode and round-trip exactly.
+        est = cb["status"]
+        good = est == 0
+        n_init = int((est == FSE_ERR_ENCODER_INIT).sum())
+        nb = codec.n_blocks(nbytes)
+        full = nbytes // block
+        ok = int(((est != 0) & (est != FSE_ERR_ENCODER_INIT)).sum()) == 0
+        if ok and bool(good.any()):
+            ok = int(st[good].abs().max()) == 0
+        if ok and bool(good.any()):
+            g = good[:full]
+            ok = bool(torch.equal(out[: full * block].view(full, block)[g], src[: full * block].view(full, block)[g]))
+            if nb > full and bool(good[full]):
+                ok = ok and bool(torch.equal(out[full * block:], src[full * block:]))
         comp = int(cb["comp_len"].to(torch.int64).sum())
-        rows.append({"dist": name, "table_log": L, "compressed_ratio": round(comp / nbytes, 4),
-                     "encode_GiB_s": round(nbytes / (enc_ms * 1e-3) / 2**30, 1),
-                     "decode_GiB_s": round(nbytes / (dec_ms * 1e-3) / 2**30, 1),
-                     "roundtrip_GiB_s": round(nbytes / ((enc_ms + dec_ms) * 1e-3) / 2**30, 1), "verified": ok})
+        row = {"dist": name, "table_log": L, "compressed_ratio": round(comp / nbytes, 4),
+               "encode_GiB_s": round(nbytes / (enc_ms * 1e-3) / 2**30, 1),
+               "decode_GiB_s": round(nbytes / (dec_ms * 1e-3) / 2**30, 1),
+               "roundtrip_GiB_s": round(nbytes / ((enc_ms + dec_ms) * 1e-3) / 2**30, 1), "verified": ok}
+        if L == 15:
+            row["note"] = "last two bytes of every block set to symbols 250, 251 (new_first_symbol panics at L=15 otherwise)"
+        if n_init:
+            row["encoder_init_blocks"] = f"{n_init}/{nb} (reference panics in new_first_symbol; rates not meaningful)"
+        rows.append(row)
         del codec, src, cb, out, st
     return rows
 
