@@ -28,6 +28,13 @@ EXPORTS = (
     "norm_histogram_write", "norm_histogram_read", "encode_table_new", "decode_table_new", "fse_compress_nh",
     "bitstack_write", "bitstack_read", "bitstream_read", "bitstream_read_ops",
     "fsehip_bitstack_write", "fsehip_bitstack_read", "fsehip_bitstream_read", "fsehip_bitstream_read_ops",
+    "bitstack_reader_new", "bitstack_reader_reload", "bitstack_reader_peek", "bitstack_reader_read_no_reload",
+    "bitstack_reader_advance_no_reload", "bitstack_reader_read", "bitstack_reader_available", "bitstack_reader_finish",
+    "bitstream_reader_new", "bitstream_reader_read", "bitstream_reader_advance_by", "bitstream_reader_peek",
+    "bitstream_reader_available", "bitstream_reader_finish", "bitstream_reader_finish_byte",
+    "bitstack_writer_new", "bitstack_writer_flush", "bitstack_writer_write_bits_raw",
+    "bitstack_writer_write_bits_raw_unmasked", "bitstack_writer_write_bits", "bitstack_writer_write_bits_unmasked",
+    "bitstack_writer_finish",
 )
 
 STATUS = {
@@ -35,6 +42,7 @@ STATUS = {
     -5: "BAD_HEADER", -6: "NO_MARKER", -7: "DST_TOO_SMALL", -8: "TABLELOG_RANGE",
     -9: "CURSED", -10: "BAD_TABLE", -11: "BAD_ARG", -12: "HIP", -13: "LENGTH_MISMATCH",
     -14: "UNSUPPORTED", -15: "NO_DEVICE", -16: "BAD_SIDECAR", -17: "ENCODER_INIT",
+    -18: "EOF",
 }
 
 
@@ -80,6 +88,23 @@ class DecodeTransform(C.Structure):
 class DecodeTable(C.Structure):
     """fse_decode_table = DecodeTable (fse.rs:253-265)."""
     _fields_ = [("table_log", C.c_uint32), ("fast_mode", C.c_uint32), ("table", DecodeTransform * 32768)]
+
+
+class BitStackReaderState(C.Structure):
+    """fse_bitstack_reader = BitStackReader (stack_reader.rs:5-11)."""
+    _fields_ = [("base", C.c_void_p), ("ptr", C.c_void_p), ("buffer", C.c_uint64), ("bits", C.c_uint64),
+                ("finished", C.c_int32), ("reserved", C.c_int32)]
+
+
+class BitStreamReaderState(C.Structure):
+    """fse_bitstream_reader = BitStreamReader (stream_reader.rs:5-11)."""
+    _fields_ = [("src", C.c_void_p), ("n", C.c_uint64), ("total_bits", C.c_uint64), ("bits_read", C.c_uint64)]
+
+
+class BitStackWriterState(C.Structure):
+    """fse_bitstack_writer = BitStackWriter (writer.rs:5-12)."""
+    _fields_ = [("dst", C.c_void_p), ("cap", C.c_uint64), ("len", C.c_uint64), ("initial_len", C.c_uint64),
+                ("storage", C.c_uint64), ("bits", C.c_uint32), ("status", C.c_int32)]
 
 
 _lib = None
@@ -137,6 +162,30 @@ def load() -> C.CDLL:
     lib.fsehip_bitstack_read.argtypes = [P, u64, P, u64, P, P, P]
     lib.fsehip_bitstream_read.argtypes = [P, u64, u64, P, u64, P, P, P]
     lib.fsehip_bitstream_read_ops.argtypes = [P, u64, u64, P, P, u64, P, P, P]
+    SR, TR, SW = C.POINTER(BitStackReaderState), C.POINTER(BitStreamReaderState), C.POINTER(BitStackWriterState)
+    pu32 = C.POINTER(u32)
+    lib.bitstack_reader_new.argtypes = [SR, P, sz]
+    lib.bitstack_reader_reload.argtypes = [SR]
+    for f in ("peek", "read_no_reload", "read"):
+        getattr(lib, "bitstack_reader_" + f).argtypes = [SR, u32, pu32]
+    lib.bitstack_reader_advance_no_reload.argtypes = [SR, u32]
+    lib.bitstack_reader_available.argtypes = [SR]
+    lib.bitstack_reader_available.restype = u64
+    lib.bitstack_reader_finish.argtypes = [SR]
+    lib.bitstream_reader_new.argtypes = [TR, P, sz, u64]
+    lib.bitstream_reader_read.argtypes = [TR, u32, pu32]
+    lib.bitstream_reader_peek.argtypes = [TR, u32, pu32]
+    lib.bitstream_reader_advance_by.argtypes = [TR, u32]
+    lib.bitstream_reader_available.argtypes = [TR]
+    lib.bitstream_reader_available.restype = u64
+    lib.bitstream_reader_finish.argtypes = [TR, C.POINTER(sz), C.POINTER(u64), pu32]
+    lib.bitstream_reader_finish_byte.argtypes = [TR]
+    lib.bitstream_reader_finish_byte.restype = sz
+    lib.bitstack_writer_new.argtypes = [SW, P, sz, sz]
+    lib.bitstack_writer_flush.argtypes = [SW]
+    for f in ("write_bits_raw", "write_bits_raw_unmasked", "write_bits", "write_bits_unmasked"):
+        getattr(lib, "bitstack_writer_" + f).argtypes = [SW, u32, u32]
+    lib.bitstack_writer_finish.argtypes = [SW, C.POINTER(sz), C.POINTER(u64)]
     lib.fsehip_device_count.argtypes = []
     lib.fsehip_version.restype = C.c_char_p
     for name in EXPORTS:

@@ -10,7 +10,8 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import (DecodeTable, EncodeTable, FseError, Histogram, NormHistogram, Params, check, load)
+from ._lib import (BitStackReaderState, BitStackWriterState, BitStreamReaderState, DecodeTable, EncodeTable, FseError,
+                   Histogram, NormHistogram, Params, check, load)
 
 
 def _buf(data) -> np.ndarray:
@@ -229,6 +230,128 @@ def bitstack_read(data, widths) -> tuple[list, int, bool]:
     return [int(x) for x in out[: nr.value]], nr.value, bool(fin.value)
 
 
+EOF_STATUS = -18  # FSE_ERR_EOF: the reference's None / Err(UnexpectedEof)
+
+
+class BitStackReader:
+    """BitStackReader (stack_reader.rs:5-227) over the C-ABI cursor
+    (fsehip.h section 1c): one O(1) call per method.  `peek` / `read` /
+    `read_no_reload` return None where the crate returns None."""
+
+    def __init__(self, data):
+        self._buf = _buf(data)  # the cursor points into this buffer
+        self.state = BitStackReaderState()
+        self._lib = load()
+        check(self._lib.bitstack_reader_new(C.byref(self.state), _p(self._buf), len(self._buf)),
+              "BitStackReader::new")
+
+    def _val(self, fn, nbits):
+        v = C.c_uint32(0)
+        rc = fn(C.byref(self.state), nbits, C.byref(v))
+        if rc == EOF_STATUS:
+            return None
+        check(rc, fn.__name__)
+        return v.value
+
+    def peek(self, nbits: int):
+        return self._val(self._lib.bitstack_reader_peek, nbits)
+
+    def read(self, nbits: int):
+        return self._val(self._lib.bitstack_reader_read, nbits)
+
+    def read_no_reload(self, nbits: int):
+        return self._val(self._lib.bitstack_reader_read_no_reload, nbits)
+
+    def advance_no_reload(self, nbits: int) -> None:
+        check(self._lib.bitstack_reader_advance_no_reload(C.byref(self.state), nbits), "advance_no_reload")
+
+    def reload(self) -> None:
+        check(self._lib.bitstack_reader_reload(C.byref(self.state)), "reload")
+
+    def available(self) -> int:
+        return int(self._lib.bitstack_reader_available(C.byref(self.state)))
+
+    def finish(self) -> bool:
+        return bool(self._lib.bitstack_reader_finish(C.byref(self.state)))
+
+
+class BitStreamReader:
+    """BitStreamReader (stream_reader.rs:5-136) over the C-ABI cursor.
+    `peek` / `read` / `advance_by` raise EOFError where the crate returns
+    Err(UnexpectedEof)."""
+
+    def __init__(self, data, total_bits: int):
+        self._buf = _buf(data)
+        self.state = BitStreamReaderState()
+        self._lib = load()
+        check(self._lib.bitstream_reader_new(C.byref(self.state), _p(self._buf), len(self._buf), total_bits),
+              "BitStreamReader::new")
+
+    def _rc(self, rc: int, what: str) -> None:
+        if rc == EOF_STATUS:
+            raise EOFError(what)
+        check(rc, what)
+
+    def peek(self, nbits: int) -> int:
+        v = C.c_uint32(0)
+        self._rc(self._lib.bitstream_reader_peek(C.byref(self.state), nbits, C.byref(v)), "peek")
+        return v.value
+
+    def read(self, nbits: int) -> int:
+        v = C.c_uint32(0)
+        self._rc(self._lib.bitstream_reader_read(C.byref(self.state), nbits, C.byref(v)), "read")
+        return v.value
+
+    def advance_by(self, nbits: int) -> None:
+        self._rc(self._lib.bitstream_reader_advance_by(C.byref(self.state), nbits), "advance_by")
+
+    def available(self) -> int:
+        return int(self._lib.bitstream_reader_available(C.byref(self.state)))
+
+    def finish(self) -> tuple[bytes, int, int]:
+        b, rem, off = C.c_size_t(0), C.c_uint64(0), C.c_uint32(0)
+        check(self._lib.bitstream_reader_finish(C.byref(self.state), C.byref(b), C.byref(rem), C.byref(off)), "finish")
+        return self._buf[b.value:].tobytes(), rem.value, off.value
+
+    def finish_byte(self) -> bytes:
+        return self._buf[int(self._lib.bitstream_reader_finish_byte(C.byref(self.state))):].tobytes()
+
+
+class BitStackWriter:
+    """BitStackWriter (writer.rs:5-223) appending to a buffer that holds
+    `prefix`, over the C-ABI cursor; `finish()` returns (the buffer's bytes,
+    bits written)."""
+
+    def __init__(self, prefix: bytes = b"", cap: int = 1 << 16):
+        self._dst = np.zeros(len(prefix) + cap, dtype=np.uint8)
+        self._dst[: len(prefix)] = np.frombuffer(bytes(prefix), dtype=np.uint8)
+        self.state = BitStackWriterState()
+        self._lib = load()
+        check(self._lib.bitstack_writer_new(C.byref(self.state), _p(self._dst), len(self._dst), len(prefix)),
+              "BitStackWriter::new")
+
+    def write_bits(self, val: int, nbits: int) -> None:
+        check(self._lib.bitstack_writer_write_bits(C.byref(self.state), val, nbits), "write_bits")
+
+    def write_bits_unmasked(self, val: int, nbits: int) -> None:
+        check(self._lib.bitstack_writer_write_bits_unmasked(C.byref(self.state), val, nbits), "write_bits_unmasked")
+
+    def write_bits_raw(self, val: int, nbits: int) -> None:
+        check(self._lib.bitstack_writer_write_bits_raw(C.byref(self.state), val, nbits), "write_bits_raw")
+
+    def write_bits_raw_unmasked(self, val: int, nbits: int) -> None:
+        check(self._lib.bitstack_writer_write_bits_raw_unmasked(C.byref(self.state), val, nbits),
+              "write_bits_raw_unmasked")
+
+    def flush(self) -> None:
+        check(self._lib.bitstack_writer_flush(C.byref(self.state)), "flush")
+
+    def finish(self) -> tuple[bytes, int]:
+        n, bits = C.c_size_t(0), C.c_uint64(0)
+        check(self._lib.bitstack_writer_finish(C.byref(self.state), C.byref(n), C.byref(bits)), "finish")
+        return self._dst[: n.value].tobytes(), bits.value
+
+
 BITS_READ, BITS_PEEK, BITS_ADVANCE = 0, 1, 2  # FSE_BITS_* (include/fsehip.h)
 
 
@@ -388,7 +511,7 @@ class BlockCodec:
         return cb["out"][s: s + ln].cpu().numpy().tobytes()
 
 
-__all__ = ["BITS_ADVANCE", "BITS_PEEK", "BITS_READ", "BlockCodec", "DecodeTable", "EncodeTable", "FseError",
+__all__ = ["BITS_ADVANCE", "BITS_PEEK", "BITS_READ", "BitStackReader", "BitStackWriter", "BitStreamReader", "BlockCodec", "DecodeTable", "EncodeTable", "FseError",
            "Histogram", "NormHistogram", "bitstack_read", "bitstack_write", "bitstream_read", "compress", "compress2",
            "compress2_log", "compress_nh", "decode_table_new", "decompress", "decompress2", "decompress_streams",
            "encode_table_new",

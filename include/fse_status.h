@@ -58,5 +58,11 @@
  * state of a symbol with norm >= 2, the u32 subtraction wraps and the
  * bounds-checked table read panics.                                         */
 #define FSE_ERR_ENCODER_INIT (-17)
+/* A bit reader ran out of bits: BitStackReader::peek/read returned None
+ * (stack_reader.rs:176-215) or BitStreamReader::peek/read/advance_by
+ * returned Err(UnexpectedEof) (stream_reader.rs:56-114).  Reported by the
+ * cursor readers of fsehip.h section 1c; the reference's callers treat it as
+ * end of stream.                                                            */
+#define FSE_ERR_EOF (-18)
 
 #endif

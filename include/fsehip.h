@@ -174,6 +174,88 @@ int bitstream_read_ops(const uint8_t* src, size_t n, uint64_t total_bits, const 
                        size_t count, uint32_t* vals, size_t* n_done, uint64_t* bits_left);
 
 /* ------------------------------------------------------------------------
+ * (1c) The bit readers and writer as incremental cursors
+ *
+ * The crate's callers drive its readers one field at a time with widths
+ * chosen from earlier values (NormHistogram::read, histogram.rs:453-496; the
+ * decoders, fse.rs:349-385).  Each reader / writer is a plain struct the
+ * caller owns (no allocation, no handle table) and every call is O(1):
+ * a Rust shim wraps it as BitStackReader / BitStreamReader / BitStackWriter
+ * with the same method names.  These run on the
+ * caller's side of the ABI (host): one field is a few shifts.  Millions of
+ * fields with known widths go through the batched device forms
+ * (fsehip_bitstack_write / fsehip_bitstack_read / fsehip_bitstream_read_ops).
+ * Semantics are the crate's on a 64-bit target (32-bit refills/flushes),
+ * including available(), which depends on the buffer's address alignment as
+ * the crate's does.  None / Err(UnexpectedEof) -> FSE_ERR_EOF; the crate's
+ * debug assertions (width > 32, advance past the buffer) -> FSE_ERR_BAD_ARG.
+ * ------------------------------------------------------------------------ */
+
+/* BitStackReader (stack_reader.rs:5-227): reads the stack from the end,
+ * after the marker bit. */
+typedef struct {
+    const uint8_t* base; /* the slice */
+    const uint8_t* ptr;  /* next refill address */
+    uint64_t buffer;
+    uint64_t bits;       /* bits buffered: available() */
+    int32_t finished;
+    int32_t reserved;
+} fse_bitstack_reader;
+/* new (stack_reader.rs:17-92): None (empty slice, zero last byte, marker not
+ * in the last byte) -> FSE_ERR_NO_MARKER */
+int bitstack_reader_new(fse_bitstack_reader* r, const uint8_t* src, size_t n);
+int bitstack_reader_reload(fse_bitstack_reader* r);                                        /* 97-172 */
+int bitstack_reader_peek(const fse_bitstack_reader* r, uint32_t nbits, uint32_t* val);      /* 176-184 */
+int bitstack_reader_read_no_reload(fse_bitstack_reader* r, uint32_t nbits, uint32_t* val); /* 193-197 */
+int bitstack_reader_advance_no_reload(fse_bitstack_reader* r, uint32_t nbits);             /* 204-207 */
+int bitstack_reader_read(fse_bitstack_reader* r, uint32_t nbits, uint32_t* val);           /* 211-215 */
+uint64_t bitstack_reader_available(const fse_bitstack_reader* r);                          /* 218-220 */
+int bitstack_reader_finish(const fse_bitstack_reader* r); /* 224-226: 1 if every bit was read */
+
+/* BitStreamReader (stream_reader.rs:5-136): forward LSB-first reader. */
+typedef struct {
+    const uint8_t* src;
+    uint64_t n;
+    uint64_t total_bits;
+    uint64_t bits_read;
+} fse_bitstream_reader;
+/* new (stream_reader.rs:16-49): n == 0 or n != ceil(total_bits/8) (the
+ * crate's asserts) -> FSE_ERR_BAD_ARG */
+int bitstream_reader_new(fse_bitstream_reader* r, const uint8_t* src, size_t n, uint64_t total_bits);
+int bitstream_reader_read(fse_bitstream_reader* r, uint32_t nbits, uint32_t* val);       /* 56-60 */
+int bitstream_reader_advance_by(fse_bitstream_reader* r, uint32_t nbits);                /* 67-75 */
+int bitstream_reader_peek(const fse_bitstream_reader* r, uint32_t nbits, uint32_t* val); /* 82-114 */
+uint64_t bitstream_reader_available(const fse_bitstream_reader* r);                      /* 117-119 */
+/* finish (123-128): the remaining slice starts at src + *byte, *remaining
+ * bits, *offset bits into its first byte */
+int bitstream_reader_finish(const fse_bitstream_reader* r, size_t* byte, uint64_t* remaining, uint32_t* offset);
+/* finish_byte (132-135): offset of the remaining bytes (next byte boundary) */
+size_t bitstream_reader_finish_byte(const fse_bitstream_reader* r);
+
+/* BitStackWriter (writer.rs:5-223) appending to dst[len..cap).  Whole bytes
+ * are committed to dst as they complete; a full buffer is a sticky
+ * FSE_ERR_DST_TOO_SMALL (the crate grows its Vec). */
+typedef struct {
+    uint8_t* dst;
+    uint64_t cap;
+    uint64_t len;         /* bytes committed (the Vec's length at finish) */
+    uint64_t initial_len;
+    uint64_t storage;     /* pending bits, LSB-first */
+    uint32_t bits;
+    int32_t status;
+} fse_bitstack_writer;
+int bitstack_writer_new(fse_bitstack_writer* w, uint8_t* dst, size_t cap, size_t len); /* 16-40 */
+int bitstack_writer_flush(fse_bitstack_writer* w);                                     /* 43-110 */
+/* write_bits_raw (164-180): val's bits above nbits must be zero; no flush */
+int bitstack_writer_write_bits_raw(fse_bitstack_writer* w, uint32_t val, uint32_t nbits);
+int bitstack_writer_write_bits_raw_unmasked(fse_bitstack_writer* w, uint32_t val, uint32_t nbits); /* 140-149 */
+int bitstack_writer_write_bits(fse_bitstack_writer* w, uint32_t val, uint32_t nbits);          /* 185-188 */
+int bitstack_writer_write_bits_unmasked(fse_bitstack_writer* w, uint32_t val, uint32_t nbits); /* 193-198 */
+/* finish (201-222): zero-pads the last byte; *dst_len = new length of dst,
+ * *bits_written = bits written since new() */
+int bitstack_writer_finish(fse_bitstack_writer* w, size_t* dst_len, uint64_t* bits_written);
+
+/* ------------------------------------------------------------------------
  * (2) Batched device entry points
  * ------------------------------------------------------------------------ */
 
