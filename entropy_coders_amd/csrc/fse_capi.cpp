@@ -333,7 +333,11 @@ static int decompress_impl(const fsehip_params* p, const uint8_t* d_in, uint64_t
     const uint64_t n_blocks = n_total ? (n_total + bs - 1) / bs : 1;
     if (n_blocks > 1 && (bs & 15u)) return FSE_ERR_BAD_ARG;
     if (n_blocks > 0xFFFFFFFFull) return FSE_ERR_BAD_ARG;
-    if (slot_bytes & 3u) return FSE_ERR_BAD_ARG;
+    // the decoders stage / read whole 16- and 32-byte chunks of a slot and
+    // store 16-byte output groups: aligned slots and buffers keep every
+    // chunk inside its slot and every access aligned
+    if ((slot_bytes & 31u) || (reinterpret_cast<uintptr_t>(d_in) & 15u) || (reinterpret_cast<uintptr_t>(d_out) & 15u))
+        return FSE_ERR_BAD_ARG;
     const uint32_t ns = p->nstates == 1 ? 1u : 2u;
     if (p->nstates > 2) return FSE_ERR_BAD_ARG;
     if ((d_sidecar || d_sidecar_out) &&
@@ -452,7 +456,8 @@ int fsehip_decompress_streams(uint32_t nstates, uint32_t max_table_log, const ui
                               uint32_t* d_out_len, int32_t* d_status, fsehip_stream_t stream) {
     if (n_streams == 0) return FSE_ERR_EMPTY;
     if (nstates > 2 || !d_in || !d_comp_len || !d_out || !d_out_len || !d_status || out_stride == 0 ||
-        (in_stride & 255u) || (reinterpret_cast<uintptr_t>(d_in) & 15u))
+        (in_stride & 255u) || (reinterpret_cast<uintptr_t>(d_in) & 15u) || (out_stride & 15u) ||
+        (reinterpret_cast<uintptr_t>(d_out) & 15u))  // 16-byte input chunks and output groups
         return FSE_ERR_BAD_ARG;
     if (max_table_log > 15) return FSE_ERR_UNSUPPORTED;
     const fsehip_params p{out_stride, 0, 0, max_table_log ? max_table_log : 11u, nstates ? nstates : 2u};

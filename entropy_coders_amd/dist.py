@@ -196,12 +196,21 @@ def scatter_stream(stream, comp_len, src: int = 0, group=None, sidecar=None, sid
     block), so every rank knows its blocks and sizes.  Step 2: `src` selects
     each rank's blocks (contiguous ranges are slices; round-robin shards go
     through fsehip_copy_blocks on the GPU) and one batch of point-to-point
-    transfers delivers them.  Other ranks pass None for stream/comp_len/sidecar.
+    transfers delivers them.  Other ranks pass None for stream/comp_len/sidecar
+    and give `device` (default: their current GPU under the nccl/RCCL
+    backend; required under gloo).
     Returns (stream, comp_len int32, sidecar or None, global block indices).
     """
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    dev = torch.device(device) if device is not None else stream.device
+    if device is not None:
+        dev = torch.device(device)
+    elif stream is not None:
+        dev = stream.device
+    elif dist.get_backend(group) == "nccl":  # RCCL moves device tensors: this rank's current GPU
+        dev = torch.device("cuda", torch.cuda.current_device())
+    else:
+        raise ValueError("scatter_stream: a rank without the stream must pass device= (gloo: 'cpu')")
     peer = (lambda r: dist.get_global_rank(group, r)) if group is not None else (lambda r: r)
     hdr = torch.zeros(3, dtype=torch.int64, device=dev)
     if rank == src:

@@ -287,8 +287,11 @@ int fsehip_compress_blocks(const fsehip_params* p, const uint8_t* d_src, uint64_
 
 /* Decompress blocks produced as above.  With d_sidecar the blocks decode in
  * parallel segments; without it (any valid fse_compress2 stream, e.g. from
- * the CPU crate) each block decodes serially, at high occupancy (its table
- * in LDS, 20 blocks in flight per CU).  n_total (> 0) gives the raw length. */
+ * the CPU crate) each block decodes serially, many at once (one lane per
+ * block, its table compact in LDS: 6 blocks per workgroup, 24 chains per
+ * CU at table log <= 11).  n_total (> 0) gives the raw length.  slot_bytes
+ * is a multiple of 256 (encoder slots are), d_in and d_out 16-byte aligned
+ * (BAD_ARG otherwise). */
 int fsehip_decompress_blocks(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
                              const uint32_t* d_comp_len, const uint64_t* d_sidecar, uint8_t* d_out,
                              uint64_t n_total, int32_t* d_status, fsehip_stream_t stream);
@@ -318,9 +321,6 @@ int fsehip_build_sidecar(const fsehip_params* p, const uint8_t* d_in, uint64_t s
                          const uint32_t* d_comp_len, uint8_t* d_out, uint64_t n_total, uint64_t* d_sidecar_out,
                          int32_t* d_status, fsehip_stream_t stream);
 
-/* Compact the slot layout into one stream (blocks back to back at the byte
- * offsets d_offsets[b], an exclusive scan of d_comp_len) and back.  Used to
- * ship compressed shards between GPUs (RCCL gather) or to the host. */
 /* Batched fse_decompress2 / fse_decompress (nstates 2 / 1) in the crate's
  * own termination (lib.rs:215-248 / 187-211), for streams with no sidecar
  * and no recorded raw length, e.g. many outputs of the CPU crate.  Stream b:
@@ -329,12 +329,21 @@ int fsehip_build_sidecar(const fsehip_params* p, const uint8_t* d_in, uint64_t s
  * out_stride, at most out_stride bytes; d_out_len[b] = bytes decoded.
  * d_status[b]: DST_TOO_SMALL when out_stride is short, SINGLE_SYMBOL for a
  * stream the crate would decode forever, UNSUPPORTED for a table log above
- * max_table_log (0 = 11; 15 accepts every stream, on slower kernels) or a
- * stream above 2^28 bytes.
+ * the kernels' bound or a stream above 2^28 bytes.  The bound is
+ * max_table_log rounded up to a kernel variant: 11 (0 = 11), 12, or 15 for
+ * 13..15 -- so max_table_log 13 or 14 accepts every stream, on the slower
+ * global-memory kernels; the decode-table workspace is 4 << bound bytes per
+ * stream (8 KiB at 11, 16 KiB at 12, 128 KiB at 15).
+ * out_stride must be a multiple of 16 and d_out 16-byte aligned (the decoder
+ * stores 16-byte groups; BAD_ARG otherwise).
  * Serial per stream, many streams at once. */
 int fsehip_decompress_streams(uint32_t nstates, uint32_t max_table_log, const uint8_t* d_in, uint64_t in_stride,
                               const uint32_t* d_comp_len, uint32_t n_streams, uint8_t* d_out, uint32_t out_stride,
                               uint32_t* d_out_len, int32_t* d_status, fsehip_stream_t stream);
+
+/* Compact the slot layout into one stream (blocks back to back at the byte
+ * offsets d_offsets[b], an exclusive scan of d_comp_len) and back.  Used to
+ * ship compressed shards between GPUs (RCCL gather) or to the host. */
 
 int fsehip_pack_blocks(const uint8_t* d_slots, uint64_t slot_bytes, const uint32_t* d_comp_len,
                        const uint64_t* d_offsets, uint32_t n_blocks, uint8_t* d_stream, fsehip_stream_t stream);

@@ -84,3 +84,22 @@ def test_building_blocks_fail_loudly_without_gpu():
         with pytest.raises(FseError) as e:
             call()
         assert e.value.code == "NO_DEVICE"
+
+
+def test_decoder_alignment_rejected_before_any_gpu_work():
+    """The decoders read whole 16/32-byte chunks of a slot and store 16-byte
+    output groups: misaligned strides or buffers are BAD_ARG up front
+    (fsehip.h), never misaligned vector accesses."""
+    import ctypes as C
+
+    lib = _lib.load()
+    ok, odd = C.c_void_p(4096), C.c_void_p(4096 + 8)
+    stat = C.c_void_p(8192)
+    # fsehip_decompress_streams: out_stride 24008 is not a multiple of 16; d_out off by 8
+    assert _lib.STATUS[lib.fsehip_decompress_streams(2, 11, ok, 256, ok, 4, ok, 24008, stat, stat, None)] == "BAD_ARG"
+    assert _lib.STATUS[lib.fsehip_decompress_streams(2, 11, ok, 256, ok, 4, odd, 24000, stat, stat, None)] == "BAD_ARG"
+    # fsehip_decompress_blocks_dt: slot not a multiple of 32, d_in or d_out misaligned
+    p = _lib.Params(65536, 0, 0, 12, 2)
+    for d_in, slot, d_out in ((ok, 90880 + 16, ok), (odd, 90880, ok), (ok, 90880, odd)):
+        rc = lib.fsehip_decompress_blocks_dt(C.byref(p), d_in, slot, ok, None, ok, ok, d_out, 65536, stat, None)
+        assert _lib.STATUS[rc] == "BAD_ARG", (d_in, slot, d_out)
