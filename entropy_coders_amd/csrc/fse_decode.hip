@@ -24,6 +24,12 @@
 #include "fse_device.hpp"
 #include "fse_kernels.h"
 
+// FSEHIP_ABL: decode ablations for A/B timing builds only
+// (tools/variant_build.sh); the product is built with 0.
+#ifndef FSEHIP_ABL
+#define FSEHIP_ABL 0
+#endif
+
 namespace fsehip {
 
 // ------------------------------------------------------------------------
@@ -213,9 +219,22 @@ struct LdsChain {
     }
     __device__ __forceinline__ uint32_t pair(const uint32_t* pay, const uint8_t* dtb) {
         const int32_t lo = (pos - 24) & ~31;
+#if FSEHIP_ABL & 1  // ablation (timing only, wrong output): conflict-free payload reads
+        const int32_t wabl = max(((lo >> 5) & ~31) + (int32_t)(__builtin_amdgcn_workitem_id_x() & 31u), 0);
+        const uint32_t w0 = pay[wabl];
+#elif FSEHIP_ABL & 10  // garbage states may run a segment below the image: stay inside it
+        const uint32_t w0 = pay[max(lo >> 5, -1)];
+#else
         const uint32_t w0 = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(pay) + (lo >> 3));
+#endif
+#if FSEHIP_ABL & 2  // ablation (timing only, wrong output): conflict-free table reads
+        const uint32_t lb = (__builtin_amdgcn_workitem_id_x() & 31u) << 2;
+        const uint32_t e0 = *reinterpret_cast<const uint32_t*>(dtb + ((a0 & ~0x7Fu) | lb));
+        const uint32_t e1 = *reinterpret_cast<const uint32_t*>(dtb + ((a1 & ~0x7Fu) | lb));
+#else
         const uint32_t e0 = *reinterpret_cast<const uint32_t*>(dtb + a0);
         const uint32_t e1 = *reinterpret_cast<const uint32_t*>(dtb + a1);
+#endif
         const uint32_t w1 = lo == B ? whi : wlo;
         pos -= (int32_t)((e0 + e1) & 0xFFu);
         const uint32_t x = (uint32_t)((((uint64_t)w1 << 32) | w0) >> (uint32_t)(pos - lo));
@@ -240,9 +259,92 @@ __device__ __forceinline__ uint32_t lds_bits32(const uint32_t* pay, int32_t pos)
 // 32 pairs = one whole 64-byte piece of output per lane, stored back to
 // back (full HBM write bursts instead of masked partial ones).
 __device__ __forceinline__ void store_group(uint8_t* __restrict__ dst, const uint32_t* w) {
+#if FSEHIP_ABL & 16  // ablation (timing only): no output stores, the values kept live
+#pragma unroll
+    for (uint32_t q = 0; q < DEC_GROUP / 8u; ++q)
+        asm volatile("; sink %0 %1 %2 %3" ::"v"(w[4 * q]), "v"(w[4 * q + 1]), "v"(w[4 * q + 2]), "v"(w[4 * q + 3]));
+    (void)dst;
+#else
     uint4* o4 = reinterpret_cast<uint4*>(dst);
 #pragma unroll
     for (uint32_t q = 0; q < DEC_GROUP / 8u; ++q) o4[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+#endif
+}
+
+// Output pieces through the wave's rows.  Lane (row r, column i) = lane
+// 16r + i holds a 64-byte piece = chunks C[0..3] of 16 bytes (w[4c..4c+3]).
+// A 4x4 transpose of (row, chunk) per column -- permlane32_swap on chunk
+// pairs (0,2), (1,3), then permlane16_swap on (0,1), (2,3) -- leaves in lane
+// (r, i), slot k, chunk r of lane (k, i)'s piece.  Store k then writes 16
+// whole pieces (4 lanes x 16 contiguous bytes each) instead of 64 lanes'
+// separate 16-byte pieces of 64 lines: 16 VALU per 32 pairs.
+__device__ __forceinline__ void rows_transpose(uint32_t* w) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const auto r = __builtin_amdgcn_permlane32_swap(w[4 * c + d], w[4 * (c + 2) + d], false, false);
+            w[4 * c + d] = r[0];
+            w[4 * (c + 2) + d] = r[1];
+        }
+#pragma unroll
+    for (int c = 0; c < 4; c += 2)
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const auto r = __builtin_amdgcn_permlane16_swap(w[4 * c + d], w[4 * (c + 1) + d], false, false);
+            w[4 * c + d] = r[0];
+            w[4 * (c + 1) + d] = r[1];
+        }
+}
+
+// Whole output groups of one chain per lane, wave-synchronous (every lane of
+// the wave runs ng_max iterations; a lane decodes only its first my_ng),
+// stored through rows_transpose: obase[k] / ong[k] are the piece base and
+// group count of lane (k, column) -- the owner of this lane's slot k.
+__device__ __forceinline__ void run_groups_tx(LdsChain& c, uint32_t my_ng, uint32_t ng_max, const uint32_t* pay,
+                                              const uint8_t* dtb, uint8_t* const* obase, const uint32_t* ong,
+                                              uint32_t row) {
+    for (uint32_t g = 0; g < ng_max; ++g) {
+        uint32_t w[DEC_GROUP / 2u];
+        if (g < my_ng) {
+#pragma unroll
+            for (uint32_t j = 0; j < DEC_GROUP; j += 2u) {
+                const uint32_t lo = c.pair(pay, dtb);
+                const uint32_t hi = c.pair(pay, dtb);
+                w[j >> 1] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+            }
+        } else {
+#pragma unroll
+            for (uint32_t j = 0; j < DEC_GROUP / 2u; ++j) w[j] = 0;
+        }
+        rows_transpose(w);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (g < ong[k])
+                *reinterpret_cast<uint4*>(obase[k] + g * 2u * DEC_GROUP + 16u * row) =
+                    make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+    }
+}
+
+// `ng` whole output groups of two independent chains, their pairs
+// interleaved (one lane, two segments: while one chain waits on its LDS
+// reads the other's arithmetic issues).
+__device__ __forceinline__ void run_chains2(LdsChain& a, LdsChain& b, const uint32_t* pay, const uint8_t* dtb,
+                                            uint32_t pa, uint32_t pb, uint32_t ng, uint8_t* __restrict__ out) {
+    for (uint32_t g = 0; g < ng; ++g) {
+        uint32_t wa[DEC_GROUP / 2u], wb[DEC_GROUP / 2u];
+#pragma unroll
+        for (uint32_t j = 0; j < DEC_GROUP; j += 2u) {
+            const uint32_t la = a.pair(pay, dtb);
+            const uint32_t lb = b.pair(pay, dtb);
+            const uint32_t ha = a.pair(pay, dtb);
+            const uint32_t hb = b.pair(pay, dtb);
+            wa[j >> 1] = __builtin_amdgcn_perm(ha, la, 0x05040100u);
+            wb[j >> 1] = __builtin_amdgcn_perm(hb, lb, 0x05040100u);
+        }
+        store_group(out + 2u * (pa + g * DEC_GROUP), wa);
+        store_group(out + 2u * (pb + g * DEC_GROUP), wb);
+    }
 }
 
 // Pairs [p, p1) of one chain, then (when `last`) the container-mode end.
@@ -347,6 +449,15 @@ __device__ __forceinline__ int32_t run_chain1(LdsChain1& c, const uint32_t* pay,
 // LMAX > 12 the table alone fills the LDS and every block reads its payload
 // through a global-memory window (pass 0).
 // ------------------------------------------------------------------------
+// Segment of thread tid in a round of 256.
+__device__ __forceinline__ uint32_t seg_of(uint32_t tid) {
+#if FSEHIP_ABL & 32  // A/B: consecutive segments on consecutive lanes
+    return tid;
+#else
+    return (tid * 33u) & 255u;
+#endif
+}
+
 template <int LMAX, uint32_t PMAX>
 struct PreSmem {
     uint32_t pad[4];  // below the image: the window may start at word -1
@@ -383,7 +494,7 @@ __global__ __launch_bounds__(256) void decode_pre_kernel(DecParams P) {
     const int32_t hdr_bits = (info & 0xFFFF) * 8;
     const uint32_t L = (uint32_t)info >> 16;
     {  // stage the block image and the table
-        if (in_lds) {
+        if (in_lds && !(FSEHIP_ABL & 8)) {  // ABL 8 (timing only): decode whatever the LDS holds
             const uint32_t nvec = (clen + 15u) >> 4;
             const uint4* src4 = reinterpret_cast<const uint4*>(in);
             uint4* dst4 = reinterpret_cast<uint4*>(sm.pay);
@@ -399,6 +510,10 @@ __global__ __launch_bounds__(256) void decode_pre_kernel(DecParams P) {
         __syncthreads();
     }
     FSE_STAMP(P, 3);
+#if FSEHIP_ABL & 4  // ablation (timing only): stage, then stop
+    if (tid == 0) P.status[gb] = FSE_OK;
+    return;
+#endif
     const uint32_t smask = (1u << L) - 1u;
     // main-loop steps: pairs (NS = 2) or symbols below the last one (NS = 1)
     const uint32_t Pm = NS == 2 ? ((n & 1u) ? (n - 3u) / 2u : n / 2u - 1u) : n - 1u;
@@ -409,8 +524,96 @@ __global__ __launch_bounds__(256) void decode_pre_kernel(DecParams P) {
     const uint8_t* dtb = reinterpret_cast<const uint8_t*>(sm.dt);
     const uint32_t* gw = reinterpret_cast<const uint32_t*>(in);
     int32_t err = FSE_OK;
-    for (uint32_t base = 0; base < nseg; base += NT) {
-        const uint32_t seg = base + (NS == 2 ? ((tid * 33u) & (NT - 1u)) : tid);
+    uint32_t base0 = 0;
+    if (NS == 2 && !BIG && in_lds) {
+        // Two segments per lane while a round has more segments than lanes
+        // (checkpoints every <= 64 pairs at 64 KiB): segments s and s + NT
+        // decoded interleaved, two independent chains per lane.
+        for (; base0 + NT < nseg; base0 += 2u * NT) {
+            const uint32_t sa = base0 + seg_of(tid), sb = sa + NT;
+            bool act[2] = {sa < nseg, sb < nseg};
+            const uint32_t sg[2] = {sa, sb};
+            LdsChain c[2];
+            uint32_t pp[2], pe[2];
+            uint64_t en[2];
+            int32_t r[2] = {FSE_OK, FSE_OK};
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                pp[k] = sg[k] * I;
+                pe[k] = min(pp[k] + I, Pm);
+                en[k] = 0;
+                if (!act[k]) continue;
+                const uint64_t e = sc[sg[k]];
+                en[k] = sg[k] == nseg - 1u ? 0ull : sc[sg[k] + 1u];
+                if ((uint32_t)e > maxbp) {  // corrupt index: never read outside the block
+                    r[k] = FSE_ERR_BAD_SIDECAR;
+                    act[k] = false;
+                    continue;
+                }
+                c[k].init(sm.pay, hdr_bits + (int32_t)(uint32_t)e, (uint32_t)(e >> 32) & smask,
+                          (uint32_t)(e >> 48) & smask);
+            }
+            const uint32_t ng = (act[0] && act[1]) ? min(pe[0] - pp[0], pe[1] - pp[1]) / DEC_GROUP : 0u;
+            run_chains2(c[0], c[1], sm.pay, dtb, pp[0], pp[1], ng, out);
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                if (!act[k]) continue;
+                const bool last = sg[k] == nseg - 1u;
+                r[k] = run_chain(c[k], sm.pay, dtb, pp[k] + ng * DEC_GROUP, pe[k], last, n, Pm, out, hdr_bits);
+                if (r[k] == FSE_OK && !last && !ckpt_match(en[k], hdr_bits, smask, c[k].pos, c[k].a0, c[k].a1))
+                    r[k] = FSE_ERR_BAD_SIDECAR;
+            }
+            if (r[0] != FSE_OK) err = r[0];
+            if (r[1] != FSE_OK) err = r[1];
+        }
+    }
+    if (NS == 2 && !BIG && in_lds) {
+        // One segment per lane, every lane of a wave in step, output pieces
+        // stored through the row transpose (run_groups_tx); then each lane's
+        // tail pairs and, for the last segment, the block's end.
+        for (; base0 < nseg; base0 += NT) {
+            const uint32_t seg = base0 + seg_of(tid);
+            bool act = seg < nseg;
+            const uint32_t p0 = seg * I, p1 = act ? min(p0 + I, Pm) : p0;
+            const bool lastseg = seg == nseg - 1u;
+            int32_t r = FSE_OK;
+            LdsChain c;
+            uint64_t en = 0;
+            if (act) {
+                const uint64_t e = sc[seg];
+                en = lastseg ? 0ull : sc[seg + 1u];
+                if ((uint32_t)e > maxbp) {  // corrupt index: never read outside the block
+                    r = FSE_ERR_BAD_SIDECAR;
+                    act = false;
+                } else {
+                    c.init(sm.pay, hdr_bits + (int32_t)(uint32_t)e, (uint32_t)(e >> 32) & smask,
+                           (uint32_t)(e >> 48) & smask);
+                }
+            }
+            const uint32_t my_ng = act ? (p1 - p0) / DEC_GROUP : 0u;
+            const uint32_t ng_max = wave_max(my_ng);
+            if (ng_max) {
+                uint8_t* obase[4];
+                uint32_t ong[4];
+#pragma unroll
+                for (uint32_t k = 0; k < 4; ++k) {
+                    const uint32_t os = base0 + seg_of((tid & ~63u) + 16u * k + (tid & 15u));
+                    const uint32_t oq = os * I;
+                    ong[k] = os < nseg ? (min(oq + I, Pm) - oq) / DEC_GROUP : 0u;
+                    obase[k] = out + 2u * oq;
+                }
+                run_groups_tx(c, my_ng, ng_max, sm.pay, dtb, obase, ong, (tid >> 4) & 3u);
+            }
+            if (act) {
+                r = run_chain(c, sm.pay, dtb, p0 + my_ng * DEC_GROUP, p1, lastseg, n, Pm, out, hdr_bits);
+                if (r == FSE_OK && !lastseg && !ckpt_match(en, hdr_bits, smask, c.pos, c.a0, c.a1))
+                    r = FSE_ERR_BAD_SIDECAR;
+            }
+            if (r != FSE_OK) err = r;
+        }
+    }
+    for (uint32_t base = base0; base < nseg; base += NT) {
+        const uint32_t seg = base + (NS == 2 ? seg_of(tid) : tid);
         if (seg >= nseg) continue;
         const uint64_t e = sc[seg];
         const uint32_t p0 = seg * I, p1 = min(p0 + I, Pm);

@@ -103,3 +103,43 @@ def test_dtables_error_blocks(torch_cuda):
     assert STATUS[int(info[1])] == "EMPTY" and stat[1] == info[1]
     assert STATUS[int(info[2])] == "NO_MARKER" and stat[2] == info[2]
     assert np.array_equal(out[:4096].cpu().numpy(), host[:4096])
+
+
+@pytest.mark.parametrize("ckpt", [64, 32])
+def test_dual_chain_segments(torch_cuda, ckpt):
+    """Checkpoints every <= 64 pairs give a 64 KiB block more segments than
+    the decoder's 256 lanes: each lane then decodes two segments
+    interleaved.  Exact against the source and the oracle's bytes, on the
+    prebuilt-table and the built-inside routes, with a ragged last block,
+    and a corrupted checkpoint is reported on the dual path."""
+    torch = torch_cuda
+    from entropy_coders_amd import BlockCodec
+    from entropy_coders_amd._lib import STATUS
+
+    codec = BlockCodec(block_size=65536, ckpt_interval=ckpt)
+    n = 40 * 65536 + 33333
+    src = codec.generate(0, 0.155, 0x5EED0009 + ckpt, n)
+    cb = codec.compress(src)
+    torch.cuda.synchronize()
+    assert int(cb["status"].abs().max()) == 0
+    host = src.cpu().numpy()
+    for b in (0, 17, 40):
+        assert codec.block_bytes(cb, b) == O.compress2(host[b * 65536:(b + 1) * 65536])[0]
+    out, st = codec.decompress(cb)
+    torch.cuda.synchronize()
+    assert int(st.abs().max()) == 0 and torch.equal(out, src)
+    tabs = codec.build_dtables(cb)
+    out2 = torch.empty_like(src)
+    st2 = torch.zeros(codec.n_blocks(n), dtype=torch.int32, device=src.device)
+    codec.decompress_dt_into(cb, tabs, out2, st2)
+    torch.cuda.synchronize()
+    assert int(st2.abs().max()) == 0 and torch.equal(out2, src)
+    # a wrong state in a checkpoint of block 5's second half (a B-chain segment)
+    spb = codec.side_per_block
+    k = 5 * spb + (32767 // ckpt + 1) * 3 // 4
+    cb["sidecar"][k] ^= 1 << 33
+    codec.decompress_dt_into(cb, tabs, out2, st2)
+    torch.cuda.synchronize()
+    stat = st2.cpu().numpy()
+    assert STATUS[int(stat[5])] == "BAD_SIDECAR"
+    assert (np.delete(stat, 5) == 0).all()
