@@ -950,7 +950,8 @@ int bitstream_read(const uint8_t* src, size_t n, uint64_t total_bits, const uint
 // Diagnostics only (not part of include/fsehip.h): resident workgroups per CU.
 int fsehipx_occupancy(char* buf, int cap) {
     if (!buf || cap <= 0 || !device_ok()) return 0;
-    return fsehip::occupancy_report(buf, cap);
+    const int n = fsehip::occupancy_report(buf, cap);
+    return n < cap ? n + fsehip::occupancy_report_dec(buf + n, cap - n) : n;
 }
 
 }  // extern "C"

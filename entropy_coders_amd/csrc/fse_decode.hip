@@ -245,7 +245,19 @@ struct LdsChain {
         const uint32_t v0 = __builtin_amdgcn_ubfe(x, e1, e0);
         a0 = (e0 >> 16) + (v0 << 2);
         a1 = (e1 >> 16) + (v1 << 2);
+#if FSEHIP_ABL & 64  // A/B (timing only): 4 extra independent VALU per pair
+        {
+            uint32_t d0 = e0 ^ 0x1234u, d1 = e1 + 77u, d2 = x * 3u, d3 = w0 | 5u;
+            asm volatile("; pad %0 %1 %2 %3" ::"v"(d0), "v"(d1), "v"(d2), "v"(d3));
+        }
+#endif
         return __builtin_amdgcn_perm(e1, e0, 0x0c0c0501u);  // sym0 | sym1 << 8
+    }
+    __device__ __forceinline__ uint32_t s0() const { return a0 >> 2; }
+    __device__ __forceinline__ uint32_t s1() const { return a1 >> 2; }
+    // decode-table entry of state s (Dte layout)
+    __device__ static __forceinline__ uint32_t entry(const uint8_t* dtb, uint32_t s) {
+        return *reinterpret_cast<const uint32_t*>(dtb + 4u * s);
     }
 };
 
@@ -301,8 +313,9 @@ __device__ __forceinline__ void rows_transpose(uint32_t* w) {
 // the wave runs ng_max iterations; a lane decodes only its first my_ng),
 // stored through rows_transpose: obase[k] / ong[k] are the piece base and
 // group count of lane (k, column) -- the owner of this lane's slot k.
-__device__ __forceinline__ void run_groups_tx(LdsChain& c, uint32_t my_ng, uint32_t ng_max, const uint32_t* pay,
-                                              const uint8_t* dtb, uint8_t* const* obase, const uint32_t* ong,
+template <class Chain, class Tab>
+__device__ __forceinline__ void run_groups_tx(Chain& c, uint32_t my_ng, uint32_t ng_max, const uint32_t* pay,
+                                              const Tab& dtb, uint8_t* const* obase, const uint32_t* ong,
                                               uint32_t row) {
     for (uint32_t g = 0; g < ng_max; ++g) {
         uint32_t w[DEC_GROUP / 2u];
@@ -329,8 +342,9 @@ __device__ __forceinline__ void run_groups_tx(LdsChain& c, uint32_t my_ng, uint3
 // `ng` whole output groups of two independent chains, their pairs
 // interleaved (one lane, two segments: while one chain waits on its LDS
 // reads the other's arithmetic issues).
-__device__ __forceinline__ void run_chains2(LdsChain& a, LdsChain& b, const uint32_t* pay, const uint8_t* dtb,
-                                            uint32_t pa, uint32_t pb, uint32_t ng, uint8_t* __restrict__ out) {
+template <class Chain, class Tab>
+__device__ __forceinline__ void run_chains2(Chain& a, Chain& b, const uint32_t* pay, const Tab& dtb, uint32_t pa,
+                                            uint32_t pb, uint32_t ng, uint8_t* __restrict__ out) {
     for (uint32_t g = 0; g < ng; ++g) {
         uint32_t wa[DEC_GROUP / 2u], wb[DEC_GROUP / 2u];
 #pragma unroll
@@ -348,9 +362,10 @@ __device__ __forceinline__ void run_chains2(LdsChain& a, LdsChain& b, const uint
 }
 
 // Pairs [p, p1) of one chain, then (when `last`) the container-mode end.
-__device__ __forceinline__ int32_t run_chain(LdsChain& c, const uint32_t* pay, const uint8_t* dtb, uint32_t p,
-                                             uint32_t p1, bool last, uint32_t n, uint32_t Pm,
-                                             uint8_t* __restrict__ out, int32_t hdr_bits) {
+template <class Chain, class Tab>
+__device__ __forceinline__ int32_t run_chain(Chain& c, const uint32_t* pay, const Tab& dtb, uint32_t p, uint32_t p1,
+                                             bool last, uint32_t n, uint32_t Pm, uint8_t* __restrict__ out,
+                                             int32_t hdr_bits) {
     for (; p + DEC_GROUP <= p1; p += DEC_GROUP) {
         uint32_t w[DEC_GROUP / 2u];
 #pragma unroll
@@ -368,9 +383,8 @@ __device__ __forceinline__ int32_t run_chain(LdsChain& c, const uint32_t* pay, c
     }
     if (!last) return FSE_OK;
     // states as indices for the shared end; the chain keeps byte offsets
-    uint32_t s0 = c.a0 >> 2, s1 = c.a1 >> 2;
-    return finish2<11>(2u * Pm, n, s0, s1, c.pos, hdr_bits, out,
-                       [&](uint32_t s) { return *reinterpret_cast<const uint32_t*>(dtb + 4u * s); },
+    uint32_t s0 = c.s0(), s1 = c.s1();
+    return finish2<11>(2u * Pm, n, s0, s1, c.pos, hdr_bits, out, [&](uint32_t s) { return Chain::entry(dtb, s); },
                        [&](uint32_t nb) {
                            c.pos -= (int32_t)nb;
                            return __builtin_amdgcn_ubfe(lds_bits32(pay, c.pos), 0u, nb);
@@ -460,19 +474,23 @@ __device__ __forceinline__ uint32_t seg_of(uint32_t tid) {
 
 template <int LMAX, uint32_t PMAX>
 struct PreSmem {
+#if FSEHIP_ABL & 128  // A/B (timing only): 30 KiB more LDS, 2 workgroups per CU
+    uint32_t occ_pad[(30u << 10) / 4];
+#endif
     uint32_t pad[4];  // below the image: the window may start at word -1
     uint32_t pay[PMAX / 4];
     uint32_t dt[1u << LMAX];
     int err[4];
 };
 
-template <int LMAX, uint32_t PMAX, int NS>
-__global__ __launch_bounds__(256) void decode_pre_kernel(DecParams P) {
+// One block (gb) by the whole workgroup; LDS reuse across calls is safe:
+// every reader of the image and table has passed the final barrier before
+// the next call's staging writes them.
+template <int LMAX, uint32_t PMAX, int NS, class Smem>
+__device__ __forceinline__ void decode_pre_block(const DecParams& P, Smem& sm, const uint64_t gb) {
     constexpr bool BIG = LMAX > 12;  // no LDS image
     constexpr uint32_t NT = 256u, NW = 4u;
-    __shared__ PreSmem<LMAX, BIG ? 16u : PMAX> sm;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-    const uint64_t gb = blockIdx.x;
     if (gb >= P.n_blocks) return;
     const uint8_t* in = P.in + gb * P.slot_bytes;
     const uint32_t clen = P.comp_len[gb];
@@ -481,13 +499,13 @@ __global__ __launch_bounds__(256) void decode_pre_kernel(DecParams P) {
     uint8_t* out = P.out + ooff;
     const int32_t info = P.dtinfo[gb];
     const bool in_lds = !BIG && clen <= PMAX;
-    if (P.pass == 2 && P.status[gb] != FSE_DEFERRED) return;  // done by the first pass
+    if (P.pass >= 2 && P.status[gb] != FSE_DEFERRED) return;  // done by an earlier pass
     FSE_STAMP(P, 0);
     if (info < 0 || n < (NS == 2 ? 2u : 1u)) {
         if (tid == 0) P.status[gb] = info < 0 ? info : FSE_ERR_LENGTH_MISMATCH;
         return;
     }
-    if (P.pass == 1 && !in_lds) {  // too big for this stage: the big-stage pass decodes it
+    if (P.pass == 1 && !in_lds) {  // too big for this stage: the list pass decodes it
         if (tid == 0) P.status[gb] = FSE_DEFERRED;
         return;
     }
@@ -503,9 +521,11 @@ __global__ __launch_bounds__(256) void decode_pre_kernel(DecParams P) {
         }
         const uint32_t dvec = 1u << L >> 2;  // 4 << L bytes
         const uint4* t4 = reinterpret_cast<const uint4*>(P.dt + gb * (uint64_t)(1u << LMAX));
-        uint4* d4 = reinterpret_cast<uint4*>(sm.dt);
-        for (uint32_t i = wv * 64u; i < dvec; i += NT)
-            if (i + lane < dvec) __builtin_amdgcn_global_load_lds(t4 + i + lane, d4 + i, 16, 0, 0);
+        {
+            uint4* d4 = reinterpret_cast<uint4*>(sm.dt);
+            for (uint32_t i = wv * 64u; i < dvec; i += NT)
+                if (i + lane < dvec) __builtin_amdgcn_global_load_lds(t4 + i + lane, d4 + i, 16, 0, 0);
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
@@ -521,6 +541,7 @@ __global__ __launch_bounds__(256) void decode_pre_kernel(DecParams P) {
     const uint32_t nseg = Pm / I + 1u;
     const uint64_t* sc = P.sidecar + gb * P.ckpt_per_block;
     const uint32_t maxbp = clen * 8u - (uint32_t)hdr_bits;
+    using Chain = LdsChain;
     const uint8_t* dtb = reinterpret_cast<const uint8_t*>(sm.dt);
     const uint32_t* gw = reinterpret_cast<const uint32_t*>(in);
     int32_t err = FSE_OK;
@@ -533,7 +554,7 @@ __global__ __launch_bounds__(256) void decode_pre_kernel(DecParams P) {
             const uint32_t sa = base0 + seg_of(tid), sb = sa + NT;
             bool act[2] = {sa < nseg, sb < nseg};
             const uint32_t sg[2] = {sa, sb};
-            LdsChain c[2];
+            Chain c[2];
             uint32_t pp[2], pe[2];
             uint64_t en[2];
             int32_t r[2] = {FSE_OK, FSE_OK};
@@ -560,7 +581,8 @@ __global__ __launch_bounds__(256) void decode_pre_kernel(DecParams P) {
                 if (!act[k]) continue;
                 const bool last = sg[k] == nseg - 1u;
                 r[k] = run_chain(c[k], sm.pay, dtb, pp[k] + ng * DEC_GROUP, pe[k], last, n, Pm, out, hdr_bits);
-                if (r[k] == FSE_OK && !last && !ckpt_match(en[k], hdr_bits, smask, c[k].pos, c[k].a0, c[k].a1))
+                if (r[k] == FSE_OK && !last &&
+                    !ckpt_match(en[k], hdr_bits, smask, c[k].pos, c[k].s0() << 2, c[k].s1() << 2))
                     r[k] = FSE_ERR_BAD_SIDECAR;
             }
             if (r[0] != FSE_OK) err = r[0];
@@ -577,7 +599,7 @@ __global__ __launch_bounds__(256) void decode_pre_kernel(DecParams P) {
             const uint32_t p0 = seg * I, p1 = act ? min(p0 + I, Pm) : p0;
             const bool lastseg = seg == nseg - 1u;
             int32_t r = FSE_OK;
-            LdsChain c;
+            Chain c;
             uint64_t en = 0;
             if (act) {
                 const uint64_t e = sc[seg];
@@ -606,7 +628,7 @@ __global__ __launch_bounds__(256) void decode_pre_kernel(DecParams P) {
             }
             if (act) {
                 r = run_chain(c, sm.pay, dtb, p0 + my_ng * DEC_GROUP, p1, lastseg, n, Pm, out, hdr_bits);
-                if (r == FSE_OK && !lastseg && !ckpt_match(en, hdr_bits, smask, c.pos, c.a0, c.a1))
+                if (r == FSE_OK && !lastseg && !ckpt_match(en, hdr_bits, smask, c.pos, c.s0() << 2, c.s1() << 2))
                     r = FSE_ERR_BAD_SIDECAR;
             }
             if (r != FSE_OK) err = r;
@@ -661,6 +683,46 @@ __global__ __launch_bounds__(256) void decode_pre_kernel(DecParams P) {
             if (sm.err[w] != FSE_OK) e2 = sm.err[w];
         P.status[gb] = e2;
         if (P.out_len) P.out_len[gb] = e2 ? 0u : n;
+    }
+}
+
+// PASS 0 (every block) / 1 (blocks the stage holds; the others are marked
+// FSE_DEFERRED): one block per workgroup, grid = blocks.  PASS 2 (the
+// 66 KiB stage, 2 workgroups per CU): a grid of about one workgroup per slot
+// on the chip; workgroup w collects the deferred blocks among w, w + G,
+// w + 2G, ... (256 status reads at once, compacted in LDS) and decodes them
+// one after the other, so a batch with few or no deferred blocks costs a few
+// microseconds instead of a full-grid launch of empty workgroups (~0.03 ms
+// per GiB).
+template <int LMAX, uint32_t PMAX, int NS, int PASS>
+__global__ __launch_bounds__(256) void decode_pre_kernel(DecParams P) {
+    constexpr bool BIG = LMAX > 12;
+    __shared__ PreSmem<LMAX, BIG ? 16u : PMAX> sm;
+    if constexpr (PASS <= 1) {
+        decode_pre_block<LMAX, PMAX, NS>(P, sm, blockIdx.x);
+    } else {
+        constexpr uint32_t NT = 256u, NW = 4u;
+        __shared__ uint32_t dlist[NT];
+        __shared__ uint32_t dcnt[NW];
+        const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+        const uint64_t G = gridDim.x;
+        for (uint64_t r0 = blockIdx.x; r0 < P.n_blocks; r0 += G * NT) {
+            const uint64_t gb = r0 + G * tid;
+            const bool d = gb < P.n_blocks && P.status[gb] == FSE_DEFERRED;
+            const uint64_t m = __ballot(d);
+            if (lane == 0) dcnt[wv] = (uint32_t)__popcll(m);
+            __syncthreads();
+            uint32_t base = 0, total = 0;
+#pragma unroll
+            for (uint32_t w = 0; w < NW; ++w) {
+                base += w < wv ? dcnt[w] : 0u;
+                total += dcnt[w];
+            }
+            if (d) dlist[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = (uint32_t)gb;
+            __syncthreads();
+            for (uint32_t i = 0; i < total; ++i) decode_pre_block<LMAX, PMAX, NS>(P, sm, dlist[i]);
+            __syncthreads();  // dlist / dcnt are rewritten by the next round
+        }
     }
 }
 
@@ -1402,30 +1464,63 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
         }
         return hipGetLastError();
     }
-    // segment-parallel: LDS = image + table (44 KiB image at L <= 11 -> 3
-    // workgroups per CU); blocks above the stage (e.g. near-uniform data,
-    // ~65 KB) are deferred to a second launch with a 66 KiB stage (2
-    // workgroups per CU) instead of the global-memory reader
+    // segment-parallel, in two passes: the 44 KiB stage (36 KiB at L = 12;
+    // 3 workgroups per CU) for the blocks it holds, then a list pass with a
+    // 66 KiB stage (2 per CU) for the deferred ones (near-uniform data,
+    // ~65 KB).  Blocks above that use the windowed global-memory reader; at
+    // L 13..15 (table 128 KiB) every block does.
     constexpr uint32_t PP = 44u << 10, PB = 66u << 10;
-    DecParams P1 = P, P2 = P;
-    P1.pass = 1;
-    P2.pass = 2;
-    auto two = [&](auto k1, auto k2) {
-        hipLaunchKernelGGL(k1, g, dim3(256), 0, stream, P1);
-        hipLaunchKernelGGL(k2, g, dim3(256), 0, stream, P2);
+    static const uint32_t cus = [] {
+        int dev = 0, n = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        return (uint32_t)n;
+    }();
+    // per_cu: workgroups per CU of a list pass (grid = one per slot on the chip)
+    auto run = [&](auto kern, uint32_t pass, uint32_t per_cu) {
+        DecParams Q = P;
+        Q.pass = pass;
+        const dim3 gq(pass <= 1 ? P.n_blocks : std::min<uint32_t>(P.n_blocks, per_cu * cus));
+        hipLaunchKernelGGL(kern, gq, dim3(256), 0, stream, Q);
     };
-    DecParams P0 = P;
-    P0.pass = 0;
     if (P.nstates == 1) {
-        if (lmax <= 11) two(decode_pre_kernel<11, PP, 1>, decode_pre_kernel<11, PB, 1>);
-        else if (lmax <= 12) two(decode_pre_kernel<12, PP - 8192, 1>, decode_pre_kernel<12, PB, 1>);
-        else hipLaunchKernelGGL((decode_pre_kernel<15, 16, 1>), g, dim3(256), 0, stream, P0);
+        if (lmax <= 11) {
+            run(decode_pre_kernel<11, PP, 1, 1>, 1, 0);
+            run(decode_pre_kernel<11, PB, 1, 2>, 2, 2);
+        } else if (lmax <= 12) {
+            run(decode_pre_kernel<12, PP - 8192, 1, 1>, 1, 0);
+            run(decode_pre_kernel<12, PB, 1, 2>, 2, 2);
+        } else {
+            run(decode_pre_kernel<15, 16, 1, 0>, 0, 0);
+        }
     } else {
-        if (lmax <= 11) two(decode_pre_kernel<11, PP, 2>, decode_pre_kernel<11, PB, 2>);
-        else if (lmax <= 12) two(decode_pre_kernel<12, PP - 8192, 2>, decode_pre_kernel<12, PB, 2>);
-        else hipLaunchKernelGGL((decode_pre_kernel<15, 16, 2>), g, dim3(256), 0, stream, P0);
+        if (lmax <= 11) {
+            run(decode_pre_kernel<11, PP, 2, 1>, 1, 0);
+            run(decode_pre_kernel<11, PB, 2, 2>, 2, 2);
+        } else if (lmax <= 12) {
+            run(decode_pre_kernel<12, PP - 8192, 2, 1>, 1, 0);
+            run(decode_pre_kernel<12, PB, 2, 2>, 2, 2);
+        } else {
+            run(decode_pre_kernel<15, 16, 2, 0>, 0, 0);
+        }
     }
     return hipGetLastError();
+}
+
+int occupancy_report_dec(char* buf, int cap) {
+    int len = 0;
+    auto one = [&](const char* name, const void* k) {
+        int nb = -1;
+        hipFuncAttributes fa{};
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 256, 0);
+        (void)hipFuncGetAttributes(&fa, k);
+        if (len < cap)
+            len += snprintf(buf + len, cap - len, "%s: %d WG/CU (lds %zu B, vgpr %d)\n", name, nb, fa.sharedSizeBytes,
+                            fa.numRegs);
+    };
+    one("decode_pre<11,45056,2,1>", reinterpret_cast<const void*>(decode_pre_kernel<11, 45056u, 2, 1>));
+    one("decode_pre<11,67584,2,2>", reinterpret_cast<const void*>(decode_pre_kernel<11, 67584u, 2, 2>));
+    return len;
 }
 
 hipError_t launch_dtables(const DtParams& P, uint32_t lmax, hipStream_t stream) {

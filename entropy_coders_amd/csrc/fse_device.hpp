@@ -102,27 +102,32 @@ __device__ __forceinline__ uint64_t lds_peers(uint32_t key, uint64_t* pm, uint64
 
 // ---------------------------------------------------------------------------
 // Histogram::new (histogram.rs:18-66): 256-bin count of one block by one
-// wave.  HSUB = 8 LDS sub-histograms (lane % 8), interleaved bin-major
-// ([bin][sub]): the 8 copies of a bin sit on 8 consecutive banks, so a
-// skewed block's same-symbol atomics neither serialise on one address nor
-// pile onto one bank.  Measured against 4 copies at a 257-word stride
-// (tools/micro/hist_bench.hip, 1 GiB): C2 0.46 -> 0.29 ms, uniform
-// 0.24 -> 0.21 ms, LUT p=0.77 0.95 -> 0.43 ms.
-// Counters are 16-bit: a bin's 8 copies are 4 words of two halves (copy c =
-// lane % 8 counts in word c / 2, half c % 2), so the increment is a per-lane
-// constant and a byte's address is one shift-or; the encoder holds 4 KiB of
-// sub-histograms instead of 8.  A copy counts at most 1/8 of a segment's
-// bytes, so segments of HIST_SEG bytes cannot overflow a half; each segment
-// is folded into the u32 counts[].
+// wave.  HS LDS sub-histograms (lane % HS), interleaved bin-major
+// ([bin][sub]): the copies of a bin sit on consecutive banks, so a skewed
+// block's same-symbol atomics neither serialise on one address nor pile
+// onto one bank.  Measured against 4 copies at a 257-word stride
+// (tools/micro/hist_bench.hip, 1 GiB): C2 0.46 -> 0.29 ms with 8 copies,
+// uniform 0.24 -> 0.21 ms, LUT p=0.77 0.95 -> 0.43 ms; 16 copies (8 KiB)
+// halve the lanes behind each counter word again (round 3).
+// Counters are 16-bit: a bin's HS copies are HS/2 words of two halves (copy
+// c = lane % HS counts in word c / 2, half c % 2), so the increment is a
+// per-lane constant and a byte's address is one shift-or.  A copy counts at
+// most 1/8 of a segment's bytes, so segments of HIST_SEG bytes cannot
+// overflow a half; each segment is folded into the u32 counts[].
 // Returns table_len (1 + largest symbol, 1 for an empty block).  counts
 // must not alias hs.
 // ---------------------------------------------------------------------------
-constexpr uint32_t HSUB = 8;
+#ifndef FSE_HSUB
+#define FSE_HSUB 16
+#endif
+constexpr uint32_t HSUB = FSE_HSUB;  // default sub-histogram count
 #ifndef FSE_HIST_U16
 #define FSE_HIST_U16 1
 #endif
 constexpr bool HIST_U16 = FSE_HIST_U16 != 0;
-constexpr uint32_t HIST_WORDS = HIST_U16 ? 256 * HSUB / 2 : 256 * HSUB;
+template <uint32_t HS>
+constexpr uint32_t hist_words() { return HIST_U16 ? 256 * HS / 2 : 256 * HS; }
+constexpr uint32_t HIST_WORDS = hist_words<HSUB>();
 constexpr uint32_t HIST_SEG = 1u << 18;
 
 // The counting loop is a call of its own (noinline): inlined, it raised the
@@ -134,15 +139,18 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const u32x4 gbl_u4;
 typedef __attribute__((address_space(1))) const uint8_t gbl_u8;
 
+template <uint32_t HS>
 __device__ __attribute__((noinline)) void wave_histogram_seg(const uint8_t* __restrict__ src_generic, uint32_t n,
                                                              uint32_t* hs_generic) {
+    static_assert(HS == 8 || HS == 16, "sub-histograms");
+    constexpr uint32_t WPB = hist_words<HS>() / 256u;  // words per bin
     const uint32_t lane = lane_id();
-    // byte address of this lane's copy: ((lane / 2) % 4) words into each bin's 4
-    lds_u32* mine = (lds_u32*)hs_generic + (HIST_U16 ? ((lane >> 1) & 3u) : (lane & 7u));
+    // byte address of this lane's copy: ((lane / 2) % (HS / 2)) words into each bin's
+    lds_u32* mine = (lds_u32*)hs_generic + (HIST_U16 ? ((lane >> 1) & (HS / 2u - 1u)) : (lane & (HS - 1u)));
     const uint32_t inc = HIST_U16 ? 1u << (16u * (lane & 1u)) : 1u;
     gbl_u8* src = (gbl_u8*)src_generic;
     auto add = [&](uint32_t byte) {
-        __hip_atomic_fetch_add(&mine[byte * (HIST_WORDS / 256u)], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(&mine[byte * WPB], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
     uint32_t done = 0;
     if ((reinterpret_cast<uintptr_t>(src_generic) & 15u) == 0) {
@@ -192,26 +200,31 @@ __device__ __attribute__((noinline)) void wave_histogram_seg(const uint8_t* __re
     for (uint32_t i = done + lane; i < n; i += WAVE) add(src[i]);
 }
 
+template <uint32_t HS = HSUB>
 __device__ inline uint32_t wave_histogram(const uint8_t* __restrict__ src, uint32_t n,
-                                          uint32_t* hs /*LDS [HIST_WORDS]*/, uint32_t* counts /*LDS[256]*/) {
+                                          uint32_t* hs /*LDS [hist_words<HS>()]*/, uint32_t* counts /*LDS[256]*/) {
+    constexpr uint32_t NW = hist_words<HS>(), Q = NW / 256u / 4u;  // uint4 per bin
     const uint32_t lane = lane_id();
     for (uint32_t s = lane; s < 256; s += WAVE) counts[s] = 0;
     uint32_t seg = 0;
     do {
-        for (uint32_t i = lane; i < HIST_WORDS; i += WAVE) hs[i] = 0;
+        for (uint32_t i = lane; i < NW; i += WAVE) hs[i] = 0;
         wave_sync();
         const uint32_t m = min(n - seg, HIST_SEG);
-        wave_histogram_seg(src + seg, m, hs);
+        wave_histogram_seg<HS>(src + seg, m, hs);
         wave_sync();
         for (uint32_t s = lane; s < 256; s += WAVE) {
-            if (HIST_U16) {
-                const uint4 q = reinterpret_cast<const uint4*>(hs)[s];
-                counts[s] += (q.x & 0xFFFFu) + (q.x >> 16) + (q.y & 0xFFFFu) + (q.y >> 16) + (q.z & 0xFFFFu) +
-                             (q.z >> 16) + (q.w & 0xFFFFu) + (q.w >> 16);
-            } else {
-                const uint4 q = reinterpret_cast<const uint4*>(hs)[2 * s], r = reinterpret_cast<const uint4*>(hs)[2 * s + 1];
-                counts[s] += q.x + q.y + q.z + q.w + r.x + r.y + r.z + r.w;
+            uint32_t c = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < Q; ++k) {
+                const uint4 q = reinterpret_cast<const uint4*>(hs)[Q * s + k];
+                if (HIST_U16)
+                    c += (q.x & 0xFFFFu) + (q.x >> 16) + (q.y & 0xFFFFu) + (q.y >> 16) + (q.z & 0xFFFFu) + (q.z >> 16) +
+                         (q.w & 0xFFFFu) + (q.w >> 16);
+                else
+                    c += q.x + q.y + q.z + q.w;
             }
+            counts[s] += c;
         }
         wave_sync();
         seg += m;

@@ -49,7 +49,7 @@ struct DecParams {
     const uint32_t* dt;     // prebuilt decode tables [n_blocks][1 << lmax] (dtable_blocks_kernel)
     const int32_t* dtinfo;  // per block: header bytes | L << 16, or < 0 = status
     uint32_t pass;          // segment decode: 0 = all blocks, 1 = defer blocks the LDS stage cannot
-                            // hold (status FSE_DEFERRED), 2 = only the deferred blocks (big stage)
+                            // hold (status FSE_DEFERRED), 2 = only the deferred blocks (list pass)
     uint32_t nstates;       // 2 = fse_compress2 blocks (default), 1 = fse_compress blocks
 };
 
@@ -103,7 +103,7 @@ hipError_t launch_bits_unpack(const uint8_t* in, uint64_t n_bytes, uint64_t tota
                               const uint64_t* total, uint32_t* vals, uint64_t* result, hipStream_t s);
 
 constexpr int kStamps = 10;  // stamp slots per workgroup
-constexpr int32_t FSE_DEFERRED = 1;  // internal block status between the two decode passes
+constexpr int32_t FSE_DEFERRED = 1;  // internal block status between the decode passes
 
 hipError_t launch_encode(const EncParams& P, uint32_t lmax, hipStream_t stream);
 hipError_t launch_dtables(const DtParams& P, uint32_t lmax, hipStream_t stream);
@@ -112,6 +112,7 @@ hipError_t launch_dtables(const DtParams& P, uint32_t lmax, hipStream_t stream);
 hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream);
 // Diagnostics: resident workgroups per CU of the main kernels, as text.
 int occupancy_report(char* buf, int cap);
+int occupancy_report_dec(char* buf, int cap);
 hipError_t launch_histogram(const uint8_t* src, uint64_t n_total, uint32_t block_size, uint32_t n_blocks,
                             uint32_t* counts, uint32_t* table_len, hipStream_t stream);
 hipError_t launch_generate(const GenParams& G, hipStream_t stream);

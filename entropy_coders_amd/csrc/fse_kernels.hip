@@ -392,12 +392,19 @@ struct EncSmem {
     static constexpr int BPW = 64 / T;
     static constexpr uint32_t SIZE = 1u << LMAX;
     // A block's stateTable and symbol transforms are built last in phase 1,
-    // so until then they hold its scratch: the sub-histograms (4 KiB) and the
-    // spread's occurrence owners (2^L bytes) live in st[b], the rank loop's
-    // peer masks (512 B) in tt[b]
-    static_assert(2u * SIZE >= HIST_WORDS * 4u, "sub-histograms fit the stateTable");
-    __attribute__((aligned(16))) uint16_t st[BPW][SIZE];
-    uint2 tt[BPW][256];
+    // so until then they hold its scratch: the sub-histograms (16 copies,
+    // 8 KiB, over st and tt when one block has the wave; 8 copies, 4 KiB,
+    // in st[b] when two blocks share it), the spread's occurrence owners
+    // (2^L bytes) in st[b], the rank loop's peer masks (512 B) in tt[b]
+    static constexpr uint32_t HS = BPW == 1 ? HSUB : 8u;
+    static_assert(BPW == 1 || 2u * SIZE >= hist_words<8>() * 4u, "sub-histograms fit the stateTable");
+    union {
+        struct {
+            __attribute__((aligned(16))) uint16_t st[BPW][SIZE];
+            uint2 tt[BPW][256];
+        };
+        __attribute__((aligned(16))) uint32_t hist[BPW == 1 ? hist_words<HS>() : 4];
+    };
     // phase-1 scratch (statistics, header, spread) and phase-2 scratch
     // (trajectories, end states, merge list) share the same LDS
     union {
@@ -445,7 +452,9 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
         const uint32_t n = (uint32_t)min((uint64_t)P.block_size, P.n_total - off);
         const uint8_t* blk = P.src + off;
         uint32_t* counts = sm.ph.p1.cnt;  // the spread reuses cnt[] after normalize
-        const uint32_t tl = wave_histogram(blk, n, reinterpret_cast<uint32_t*>(sm.st[b]), counts);
+        using Sm = EncSmem<LMAX, T>;
+        const uint32_t tl = wave_histogram<Sm::HS>(
+            blk, n, BPW == 1 ? sm.hist : reinterpret_cast<uint32_t*>(sm.st[b]), counts);
         FSE_STAMP(P, 1);
         if (P.debug & 8u) {  // ablation: histogram only
             if (lane == 0) P.status[gb] = (int32_t)tl;

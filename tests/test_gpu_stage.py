@@ -1,9 +1,10 @@
 """GPU parity for the decode stage split (decode_pre_kernel
 "Oversized blocks"): blocks whose compressed image exceeds the 44 KiB LDS
-stage are deferred by the first launch and decoded by a 66 KiB-stage second
-launch; blocks above that use the global-memory reader. A batch that mixes
-all three kinds must still decode every block bit-exact, in both formats, and
-the encoded bytes must equal the oracle's (lib.rs:112-143, lib.rs:148-185).
+stage are deferred by the first launch and decoded by the 66 KiB-stage list
+pass; blocks above that use the global-memory reader. A batch that mixes
+every kind (including blocks just below and above the stage sizes) must
+still decode every block bit-exact, in both formats, and the encoded bytes
+must equal the oracle's (lib.rs:112-143, lib.rs:148-185).
 """
 import numpy as np
 import pytest
@@ -55,8 +56,10 @@ def _check(torch, codec, src, n_check):
     return lens
 
 
-# uniform (~65 KB compressed: second pass), skewed (~8 KB: first pass), C2 (~33 KB)
-LAYOUT = [(2, 0.0), (0, 0.77), (0, 0.155), (2, 0.0), (2, 0.0), (0, 0.155), (1, 0.5), (2, 0.0)]
+# uniform (~65 KB compressed: list pass), skewed (~8 KB), C2 (~33 KB) and
+# LUT p = 0.1 (~38.6 KB): first pass
+LAYOUT = [(2, 0.0), (0, 0.77), (0, 0.155), (2, 0.0), (0, 0.1), (2, 0.0), (0, 0.155), (1, 0.5), (2, 0.0)]
+MID = (34560, 44 << 10)
 
 
 @pytest.mark.parametrize("nstates", [2, 1])
@@ -66,7 +69,8 @@ def test_mixed_stage_batch(torch_cuda, nstates):
     codec = BlockCodec(block_size=65536, ckpt_interval=128 if nstates == 2 else 64, nstates=nstates)
     src = _mixed_src(torch_cuda, codec, LAYOUT * 4)
     lens = _check(torch_cuda, codec, src, len(LAYOUT))
-    assert (lens > 44 << 10).any() and (lens < 44 << 10).any()
+    assert (lens > 44 << 10).any() and (lens < 34560).any()
+    assert ((lens > MID[0]) & (lens <= MID[1])).any()
 
 
 @pytest.mark.parametrize("nstates", [2, 1])
@@ -80,3 +84,16 @@ def test_blocks_above_big_stage(torch_cuda, nstates):
     lens = _check(torch_cuda, codec, src, 4)
     assert lens.max() > 66 << 10
     assert np.count_nonzero(lens > 66 << 10) == 2
+
+
+def test_deferred_pass_many_blocks(torch_cuda):
+    """More blocks than the deferred pass has workgroups (2 per CU, ~512):
+    each of its workgroups collects and decodes several deferred blocks of
+    the strided set it scans, interleaved with blocks the first pass did."""
+    from entropy_coders_amd import BlockCodec
+
+    codec = BlockCodec(block_size=65536, ckpt_interval=128)
+    src = _mixed_src(torch_cuda, codec, LAYOUT * 140)  # 1260 blocks, 700 deferred
+    lens = _check(torch_cuda, codec, src, 3)
+    assert np.count_nonzero(lens > 44 << 10) == 560
+    assert np.count_nonzero((lens > MID[0]) & (lens <= MID[1])) == 140
