@@ -1087,89 +1087,102 @@ __device__ __forceinline__ void lds_store_release(int32_t* p, int32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// The sidecar-less decoder's table in LDS, per block: u16 entries
-// nb | newState << NBW plus a u8 symbol array, 3 bytes per state (6 KiB at
-// L = 11, 12 KiB at L = 12, against 8 / 16 KiB of dtable_blocks_kernel's u32
-// entries), so with 512-byte rings 6 blocks fit a 40 KB workgroup at
-// L <= 11 and 3 at L = 12 (4 workgroups per CU).
-// NBW = 5 (L <= 11): nb < 16 leaves bit 4 clear, so v_bfe takes the entries
-// themselves as width / offset operands and e >> 4 is the byte offset of
-// entry newState.  NBW = 4 (L = 12, newState needs 12 bits): nb is masked
-// out (e & 15) and the offset is (e >> 3) & ~1.
+typedef __attribute__((address_space(3))) const uint16_t lds_cu16;
+typedef __attribute__((address_space(3))) const uint8_t lds_cu8;
+typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
+__device__ __forceinline__ uint32_t lds_u16_at(uint32_t a) { return *(lds_cu16*)(uintptr_t)a; }
+__device__ __forceinline__ uint32_t lds_u8_at(uint32_t a) { return *(lds_cu8*)(uintptr_t)a; }
+__device__ __forceinline__ uint32_t lds_u32_at(uint32_t a) { return *(lds_cu32*)(uintptr_t)a; }
+template <class T>
+__device__ __forceinline__ uint32_t lds_addr(T* p) {
+    return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) T*)p;
+}
+
+// The sidecar-less decoder's tables in LDS: for the K blocks of a
+// workgroup, u16 entries nb | newState << NBW (ent[K][2^LMAX]) followed by
+// u8 symbols (sym[K][2^LMAX]), 3 bytes per state (6 KiB at L = 11, 12 KiB
+// at L = 12, against 8 / 16 KiB of dtable_blocks_kernel's u32 entries), so
+// with 528-byte rings 6 blocks fit a 40 KB workgroup at L <= 11 and 3 at
+// L = 12 (4 workgroups per CU).  A chain's state is its entry's LDS byte
+// address halved, B = H + state (H = its entry table / 2): the entry is at
+// 2B and the symbol at B + SO, SO = sym - ent / 2 being the same for every
+// chain (the ds_read's immediate offset), and the next state is
+// H + newState + bits (one add3).
+// NBW = 5 (L <= 11): nb < 16 leaves bit 4 clear, so the entry is the v_bfe
+// width as it is and -e its offset below the top.  NBW = 4 (L = 12,
+// newState needs 12 bits): nb = e & 15.  newState = e >> NBW.
 template <uint32_t NBW>
 struct RingTab {
     static_assert(NBW == 4 || NBW == 5, "nb field width");
-    const uint8_t* ent;  // entries
-    const uint8_t* sym;  // symbols
-    __device__ __forceinline__ uint32_t entry_at(uint32_t a) const {  // a = byte offset
-        return (uint32_t)*reinterpret_cast<const uint16_t*>(ent + a);
-    }
-    __device__ __forceinline__ uint32_t sym_at(uint32_t a) const { return (uint32_t)sym[a >> 1]; }
+    uint32_t H;   // this chain's entry table (LDS byte address) / 2
+    uint32_t SO;  // symbol of state B: LDS byte B + SO
+    __device__ __forceinline__ uint32_t entry_at(uint32_t B) const { return lds_u16_at(B << 1); }
+    __device__ __forceinline__ uint32_t sym_at(uint32_t B) const { return ((lds_cu8*)(uintptr_t)B)[SO]; }
     // nb as a bit-field operand (v_bfe reads its low five bits)
     __device__ __forceinline__ uint32_t nbf(uint32_t e) const { return NBW == 5 ? e : e & 15u; }
-    // byte offset of entry newState
-    __device__ __forceinline__ uint32_t base(uint32_t e) const { return NBW == 5 ? e >> 4 : (e >> 3) & ~1u; }
+    __device__ __forceinline__ uint32_t ns(uint32_t e) const { return e >> NBW; }
     // by state index (end-of-block steps)
-    __device__ __forceinline__ uint32_t nb(uint32_t s) const { return entry_at(s << 1) & ((1u << NBW) - 1u); }
-    __device__ __forceinline__ uint32_t symbol(uint32_t s) const { return (uint32_t)sym[s]; }
-    __device__ __forceinline__ uint32_t next_base(uint32_t s) const { return base(entry_at(s << 1)) >> 1; }
+    __device__ __forceinline__ uint32_t nb(uint32_t s) const { return entry_at(H + s) & ((1u << NBW) - 1u); }
+    __device__ __forceinline__ uint32_t symbol(uint32_t s) const { return sym_at(H + s); }
+    __device__ __forceinline__ uint32_t next_base(uint32_t s) const { return ns(entry_at(H + s)); }
 };
 
-// LdsChain over the ring.  NS = 2: a pair (<= 24 bits) per step; NS = 1:
-// one symbol (<= 12 bits).  The window [lo, lo + 64) covers the step's bits
-// and lo moves down by at most one word per step, so the upper word is
-// either the previous upper word or the previous lower one.  a0 / a1 are
-// the states' entry byte offsets.
+// Ring of one chain: RING_WORDS words of the payload by word index mod
+// RING_WORDS, plus a mirror of slot 0 in slot RING_WORDS, so that words
+// (q, q + 1) are always two adjacent slots (one ds_read2_b32).
+constexpr uint32_t RING_STRIDE = RING_WORDS + 4u;
+
+// A serial chain over its ring.  NS = 2: a pair (<= 24 bits) per step;
+// NS = 1: one symbol.  Each step reads x = the 32 payload bits just below
+// pos (words (pos - 32) / 32 and the one above, issued together with the
+// table reads: they depend only on pos), then takes decoder 0's nb0 bits
+// from the top of x and decoder 1's nb1 bits below them (stack order,
+// lib.rs:227-234) as bit fields at 32 - nb0 and 32 - nb0 - nb1: from a
+// table read back to the next one is four VALU (negate, bfe, add3, shift)
+// and no 64-bit shift or window bookkeeping.
 template <int NS, uint32_t NBW>
 struct RingChain {
-    static constexpr int32_t OFF = 12 * NS;
     using Tab = RingTab<NBW>;
-    int32_t pos, B;
-    uint32_t whi, wlo, a0, a1;
-    __device__ __forceinline__ void init(const uint32_t* ring, int32_t p, uint32_t s0, uint32_t s1) {
-        pos = p;
-        a0 = s0 << 1;
-        a1 = s1 << 1;
-        B = (p - OFF) & ~31;
-        wlo = 0;
-        whi = ring[((uint32_t)(B >> 5) + 1u) & RING_MASK];
+    int32_t p32;      // bit position - 32
+    uint32_t B0, B1;  // states as halved entry addresses
+    uint32_t R;       // this chain's ring (LDS byte address)
+    __device__ __forceinline__ void init(uint32_t ring, const Tab& T, int32_t p, uint32_t s0, uint32_t s1) {
+        p32 = p - 32;
+        R = ring;
+        B0 = T.H + s0;
+        B1 = T.H + s1;
     }
-    __device__ __forceinline__ uint32_t s0() const { return a0 >> 1; }
-    __device__ __forceinline__ uint32_t s1() const { return a1 >> 1; }
+    __device__ __forceinline__ int32_t pos() const { return p32 + 32; }
+    __device__ __forceinline__ uint32_t s0(const Tab& T) const { return B0 - T.H; }
+    __device__ __forceinline__ uint32_t s1(const Tab& T) const { return B1 - T.H; }
+    // the 32 bits [pos - 32, pos); below bit 0 (pos < 32) the low bits are
+    // stale ring contents that no step uses
+    __device__ __forceinline__ uint32_t window() const {
+        const uint32_t a = R + (__builtin_amdgcn_ubfe((uint32_t)p32, 5u, 7u) << 2);
+        return __builtin_amdgcn_alignbit(lds_u32_at(a + 4u), lds_u32_at(a), (uint32_t)p32);
+    }
     // one pair; returns sym0 | sym1 << 8
-    __device__ __forceinline__ uint32_t pair(const uint32_t* ring, const Tab& T) {
-        const int32_t lo = (pos - OFF) & ~31;
-        const uint32_t w0 = ring[(uint32_t)(lo >> 5) & RING_MASK];
-        const uint32_t e0 = T.entry_at(a0);
-        const uint32_t e1 = T.entry_at(a1);
-        const uint32_t y0 = T.sym_at(a0), y1 = T.sym_at(a1);
-        const uint32_t w1 = lo == B ? whi : wlo;
+    __device__ __forceinline__ uint32_t pair(const Tab& T) {
+        const uint32_t e0 = T.entry_at(B0), e1 = T.entry_at(B1);
+        const uint32_t y0 = T.sym_at(B0), y1 = T.sym_at(B1);
+        const uint32_t x = window();
         const uint32_t n0 = T.nbf(e0), n1 = T.nbf(e1);
-        pos -= (int32_t)((n0 + n1) & 31u);
-        const uint32_t x = (uint32_t)((((uint64_t)w1 << 32) | w0) >> (uint32_t)(pos - lo));
-        B = lo;
-        whi = w1;
-        wlo = w0;
-        const uint32_t v1 = __builtin_amdgcn_ubfe(x, 0u, n1);
-        const uint32_t v0 = __builtin_amdgcn_ubfe(x, n1, n0);
-        a0 = T.base(e0) + (v0 << 1);
-        a1 = T.base(e1) + (v1 << 1);
+        const uint32_t o0 = 0u - n0;
+        const uint32_t v0 = __builtin_amdgcn_ubfe(x, o0, n0);
+        const uint32_t v1 = __builtin_amdgcn_ubfe(x, o0 - n1, n1);
+        p32 -= (int32_t)((n0 + n1) & 31u);
+        B0 = T.H + T.ns(e0) + v0;
+        B1 = T.H + T.ns(e1) + v1;
         return y0 | (y1 << 8);
     }
     // NS = 1: one symbol; returns it
-    __device__ __forceinline__ uint32_t step(const uint32_t* ring, const Tab& T) {
-        const int32_t lo = (pos - OFF) & ~31;
-        const uint32_t w0 = ring[(uint32_t)(lo >> 5) & RING_MASK];
-        const uint32_t e = T.entry_at(a0);
-        const uint32_t y = T.sym_at(a0);
-        const uint32_t w1 = lo == B ? whi : wlo;
+    __device__ __forceinline__ uint32_t step(const Tab& T) {
+        const uint32_t e = T.entry_at(B0);
+        const uint32_t y = T.sym_at(B0);
+        const uint32_t x = window();
         const uint32_t n0 = T.nbf(e);
-        pos -= (int32_t)(n0 & 31u);
-        const uint32_t x = (uint32_t)((((uint64_t)w1 << 32) | w0) >> (uint32_t)(pos - lo));
-        B = lo;
-        whi = w1;
-        wlo = w0;
-        a0 = T.base(e) + (__builtin_amdgcn_ubfe(x, 0u, n0) << 1);
+        p32 -= (int32_t)(n0 & 31u);
+        B0 = T.H + T.ns(e) + __builtin_amdgcn_ubfe(x, 0u - n0, n0);
         return y;
     }
 };
@@ -1180,9 +1193,9 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
     static_assert(K >= 1 && K <= 64, "one decode lane per block");
     constexpr uint32_t NBW = LMAX <= 11 ? 5u : 4u;  // nb | newState << NBW fits 16 bits
     constexpr uint32_t TW = 1u << LMAX;
-    constexpr uint32_t TAB_BYTES = 3u * TW;  // per block: u16 entries + u8 symbols
-    __shared__ __attribute__((aligned(16))) uint8_t tab_all[K * TAB_BYTES];
-    __shared__ uint32_t ring_all[K * RING_WORDS];
+    // u16 entries of the K blocks, then their u8 symbols
+    __shared__ __attribute__((aligned(16))) uint8_t tab_all[K * 3u * TW];
+    __shared__ uint32_t ring_all[K * RING_STRIDE];
     __shared__ int32_t ctl_all[K][2];  // [0] lowest word landed, [1] highest word the decoder may still read; INT32_MIN = stop
     __shared__ uint32_t any_nb[K];
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
@@ -1203,7 +1216,8 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
         if (info < 0) continue;
         const uint32_t nv = (1u << ((uint32_t)info >> 16)) >> 2;
         const uint4* t4 = reinterpret_cast<const uint4*>(P.dt + gb * (uint64_t)TW);
-        uint8_t* tb = tab_all + j * TAB_BYTES;
+        uint8_t* tb = tab_all + j * 2u * TW;         // entries
+        uint8_t* sb = tab_all + K * 2u * TW + j * TW;  // symbols
         uint32_t nbor = 0;
         for (uint32_t i = tid; i < nv; i += 128u) {
             const uint4 q = t4[i];
@@ -1212,7 +1226,7 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
             auto c16 = [](uint32_t e) { return (e & 0xFu) | ((e >> (18u - NBW)) & ~((1u << NBW) - 1u)); };
             reinterpret_cast<uint2*>(tb)[i] =
                 make_uint2(c16(q.x) | (c16(q.y) << 16), c16(q.z) | (c16(q.w) << 16));
-            reinterpret_cast<uint32_t*>(tb + 2u * TW)[i] =
+            reinterpret_cast<uint32_t*>(sb)[i] =
                 __builtin_amdgcn_perm(__builtin_amdgcn_perm(q.w, q.z, 0x0c0c0501u),
                                       __builtin_amdgcn_perm(q.y, q.x, 0x0c0c0501u), 0x05040100u);
             nbor |= (q.x | q.y | q.z | q.w) & 0xFFu;
@@ -1256,9 +1270,11 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
                 }
 #pragma unroll
                 for (int32_t q = 0; q < (int32_t)(RING_WORDS / RING_CHUNK); ++q)
-                    if (k[j] - q > k1)
-                        ring_all[j * RING_WORDS +
-                                 ((uint32_t)((k[j] - q) * (int32_t)RING_CHUNK + (int32_t)lane) & RING_MASK)] = v[q];
+                    if (k[j] - q > k1) {
+                        const uint32_t slot = (uint32_t)((k[j] - q) * (int32_t)RING_CHUNK + (int32_t)lane) & RING_MASK;
+                        ring_all[j * RING_STRIDE + slot] = v[q];
+                        if (slot == 0u) ring_all[j * RING_STRIDE + RING_WORDS] = v[q];  // the mirror
+                    }
                 k[j] = k1;
                 if (lane == 0) lds_store_release(&ctl_all[j][0], (k1 + 1) * (int32_t)RING_CHUNK);
                 if (k1 < 0) act &= ~(1u << j);
@@ -1272,8 +1288,9 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
     if (lane >= K || gb >= P.n_blocks) return;
 
     // wave 0, lane j < K: the decoder of block gb0 + j
-    const RingTab<NBW> T{tab_all + lane * TAB_BYTES, tab_all + lane * TAB_BYTES + 2u * TW};
-    const uint32_t* const ring = ring_all + lane * RING_WORDS;
+    const uint32_t tab0 = lds_addr(tab_all);  // even (16-byte aligned)
+    const RingTab<NBW> T{(tab0 >> 1) + lane * TW, K * 2u * TW + (tab0 >> 1)};
+    const uint32_t* const ring = ring_all + lane * RING_STRIDE;
     int32_t* const ctl = ctl_all[lane];
     const int32_t info = P.dtinfo[gb];
     const uint8_t* in = P.in + gb * P.slot_bytes;
@@ -1316,7 +1333,7 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
         const uint32_t s0i = bits_at(top - (int32_t)L) & ((1u << L) - 1u);
         const uint32_t s1i = NS == 2 ? bits_at(top - 2 * (int32_t)L) & ((1u << L) - 1u) : 0u;
         RingChain<NS, NBW> c;
-        c.init(ring, top - NS * (int32_t)L, s0i, s1i);
+        c.init(lds_addr(ring), T, top - NS * (int32_t)L, s0i, s1i);
         const uint32_t I = P.ckpt_interval;
         uint64_t* rec = (P.sidecar_out && I) ? P.sidecar_out + gb * P.ckpt_per_block : nullptr;
         // checkpoint before pair (NS = 2) / symbol (NS = 1) pidx: bit position
@@ -1334,19 +1351,19 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
         auto bulk = [&](auto rec_on) {
             constexpr bool REC = decltype(rec_on)::value;
             auto record = [&]() {
-                if (REC) record_at(c.pos, c.s0(), c.s1());
+                if (REC) record_at(c.pos(), c.s0(T), c.s1(T));
             };
-            while (o + 18u < lim && c.pos - hdr_bits >= 16 * (int32_t)L) {
-                wait_words((c.pos - NS * 12 - 16 * (int32_t)L) >> 5);
+            while (o + 18u < lim && c.pos() - hdr_bits >= 16 * (int32_t)L) {
+                wait_words((c.pos() - 32 - 16 * (int32_t)L) >> 5);
                 uint32_t w[4];
                 if constexpr (NS == 2) {
 #pragma unroll
                     for (uint32_t j = 0; j < 8u; j += 2u) {
                         record();
-                        const uint32_t lo = c.pair(ring, T);
+                        const uint32_t lo = c.pair(T);
                         ++pidx;
                         record();
-                        const uint32_t hi = c.pair(ring, T);
+                        const uint32_t hi = c.pair(T);
                         ++pidx;
                         w[j >> 1] = lo | (hi << 16);
                     }
@@ -1357,7 +1374,7 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
 #pragma unroll
                         for (uint32_t q = 0; q < 4u; ++q) {
                             record();
-                            y |= c.step(ring, T) << (8u * q);
+                            y |= c.step(T) << (8u * q);
                             ++pidx;
                         }
                         w[j] = y;
@@ -1365,7 +1382,7 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
                 }
                 *reinterpret_cast<uint4*>(out + o) = make_uint4(w[0], w[1], w[2], w[3]);
                 o += 16;
-                lds_store_volatile(&ctl[1], (c.pos - NS * 12) >> 5);
+                lds_store_volatile(&ctl[1], c.pos() >> 5);  // the highest word a later step reads
             }
         };
         if (rec) bulk(std::true_type{});
@@ -1374,10 +1391,10 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
         // (bulk stopped by the position) or within 18 steps (stopped by the
         // output limit): wait for just those words, the loader cannot pass
         // the ring's words above what the decoder still reads
-        lds_store_volatile(&ctl[1], (c.pos >> 5) + 1);
-        wait_words(max(hdr_bits, c.pos - 20 * (int32_t)L) >> 5);
-        uint32_t s0 = c.s0(), s1 = c.s1();
-        int32_t pos = c.pos;
+        lds_store_volatile(&ctl[1], (c.pos() >> 5) + 1);
+        wait_words(max(hdr_bits, c.pos() - 20 * (int32_t)L) >> 5);
+        uint32_t s0 = c.s0(T), s1 = c.s1(T);
+        int32_t pos = c.pos();
         auto pop = [&](uint32_t nb) -> uint32_t {
             pos -= (int32_t)nb;
             return bits_at(pos) & ((1u << nb) - 1u);
