@@ -464,15 +464,16 @@ __device__ __forceinline__ int32_t run_chain1(LdsChain1& c, const uint32_t* pay,
 // through a global-memory window (pass 0).
 // ------------------------------------------------------------------------
 // Segment of thread tid in a round of 256.
+template <uint32_t NT = 256u>
 __device__ __forceinline__ uint32_t seg_of(uint32_t tid) {
 #if FSEHIP_ABL & 32  // A/B: consecutive segments on consecutive lanes
     return tid;
 #else
-    return (tid * 33u) & 255u;
+    return (tid * 33u) & (NT - 1u);  // a bijection of [0, NT): 33 is odd
 #endif
 }
 
-template <int LMAX, uint32_t PMAX>
+template <int LMAX, uint32_t PMAX, uint32_t NW = 4u>
 struct PreSmem {
 #if FSEHIP_ABL & 128  // A/B (timing only): 30 KiB more LDS, 2 workgroups per CU
     uint32_t occ_pad[(30u << 10) / 4];
@@ -480,16 +481,16 @@ struct PreSmem {
     uint32_t pad[4];  // below the image: the window may start at word -1
     uint32_t pay[PMAX / 4];
     uint32_t dt[1u << LMAX];
-    int err[4];
+    int err[NW];
 };
 
 // One block (gb) by the whole workgroup; LDS reuse across calls is safe:
 // every reader of the image and table has passed the final barrier before
 // the next call's staging writes them.
-template <int LMAX, uint32_t PMAX, int NS, class Smem>
+template <int LMAX, uint32_t PMAX, int NS, uint32_t NT, class Smem>
 __device__ __forceinline__ void decode_pre_block(const DecParams& P, Smem& sm, const uint64_t gb) {
     constexpr bool BIG = LMAX > 12;  // no LDS image
-    constexpr uint32_t NT = 256u, NW = 4u;
+    constexpr uint32_t NW = NT / 64u;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     if (gb >= P.n_blocks) return;
     const uint8_t* in = P.in + gb * P.slot_bytes;
@@ -551,7 +552,7 @@ __device__ __forceinline__ void decode_pre_block(const DecParams& P, Smem& sm, c
         // (checkpoints every <= 64 pairs at 64 KiB): segments s and s + NT
         // decoded interleaved, two independent chains per lane.
         for (; base0 + NT < nseg; base0 += 2u * NT) {
-            const uint32_t sa = base0 + seg_of(tid), sb = sa + NT;
+            const uint32_t sa = base0 + seg_of<NT>(tid), sb = sa + NT;
             bool act[2] = {sa < nseg, sb < nseg};
             const uint32_t sg[2] = {sa, sb};
             Chain c[2];
@@ -594,7 +595,7 @@ __device__ __forceinline__ void decode_pre_block(const DecParams& P, Smem& sm, c
         // stored through the row transpose (run_groups_tx); then each lane's
         // tail pairs and, for the last segment, the block's end.
         for (; base0 < nseg; base0 += NT) {
-            const uint32_t seg = base0 + seg_of(tid);
+            const uint32_t seg = base0 + seg_of<NT>(tid);
             bool act = seg < nseg;
             const uint32_t p0 = seg * I, p1 = act ? min(p0 + I, Pm) : p0;
             const bool lastseg = seg == nseg - 1u;
@@ -619,7 +620,7 @@ __device__ __forceinline__ void decode_pre_block(const DecParams& P, Smem& sm, c
                 uint32_t ong[4];
 #pragma unroll
                 for (uint32_t k = 0; k < 4; ++k) {
-                    const uint32_t os = base0 + seg_of((tid & ~63u) + 16u * k + (tid & 15u));
+                    const uint32_t os = base0 + seg_of<NT>((tid & ~63u) + 16u * k + (tid & 15u));
                     const uint32_t oq = os * I;
                     ong[k] = os < nseg ? (min(oq + I, Pm) - oq) / DEC_GROUP : 0u;
                     obase[k] = out + 2u * oq;
@@ -635,7 +636,7 @@ __device__ __forceinline__ void decode_pre_block(const DecParams& P, Smem& sm, c
         }
     }
     for (uint32_t base = base0; base < nseg; base += NT) {
-        const uint32_t seg = base + (NS == 2 ? seg_of(tid) : tid);
+        const uint32_t seg = base + (NS == 2 ? seg_of<NT>(tid) : tid);
         if (seg >= nseg) continue;
         const uint64_t e = sc[seg];
         const uint32_t p0 = seg * I, p1 = min(p0 + I, Pm);
@@ -660,7 +661,7 @@ __device__ __forceinline__ void decode_pre_block(const DecParams& P, Smem& sm, c
                     r = FSE_ERR_BAD_SIDECAR;
             }
         } else if (!BIG && in_lds) {
-            LdsChain c;
+            Chain c;
             c.init(sm.pay, hdr_bits + (int32_t)bp, s0, s1);
             r = run_chain(c, sm.pay, dtb, p0, p1, lastseg, n, Pm, out, hdr_bits);
             if (r == FSE_OK && !lastseg && !ckpt_match(en, hdr_bits, smask, c.pos, c.a0, c.a1)) r = FSE_ERR_BAD_SIDECAR;
@@ -694,14 +695,14 @@ __device__ __forceinline__ void decode_pre_block(const DecParams& P, Smem& sm, c
 // one after the other, so a batch with few or no deferred blocks costs a few
 // microseconds instead of a full-grid launch of empty workgroups (~0.03 ms
 // per GiB).
-template <int LMAX, uint32_t PMAX, int NS, int PASS>
-__global__ __launch_bounds__(256) void decode_pre_kernel(DecParams P) {
+template <int LMAX, uint32_t PMAX, int NS, int PASS, uint32_t NT = 256u>
+__global__ __launch_bounds__(NT) void decode_pre_kernel(DecParams P) {
     constexpr bool BIG = LMAX > 12;
-    __shared__ PreSmem<LMAX, BIG ? 16u : PMAX> sm;
+    constexpr uint32_t NW = NT / 64u;
+    __shared__ PreSmem<LMAX, BIG ? 16u : PMAX, NW> sm;
     if constexpr (PASS <= 1) {
-        decode_pre_block<LMAX, PMAX, NS>(P, sm, blockIdx.x);
+        decode_pre_block<LMAX, PMAX, NS, NT>(P, sm, blockIdx.x);
     } else {
-        constexpr uint32_t NT = 256u, NW = 4u;
         __shared__ uint32_t dlist[NT];
         __shared__ uint32_t dcnt[NW];
         const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
@@ -720,7 +721,7 @@ __global__ __launch_bounds__(256) void decode_pre_kernel(DecParams P) {
             }
             if (d) dlist[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = (uint32_t)gb;
             __syncthreads();
-            for (uint32_t i = 0; i < total; ++i) decode_pre_block<LMAX, PMAX, NS>(P, sm, dlist[i]);
+            for (uint32_t i = 0; i < total; ++i) decode_pre_block<LMAX, PMAX, NS, NT>(P, sm, dlist[i]);
             __syncthreads();  // dlist / dcnt are rewritten by the next round
         }
     }
@@ -1494,12 +1495,19 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
         return (uint32_t)n;
     }();
     // per_cu: workgroups per CU of a list pass (grid = one per slot on the chip)
-    auto run = [&](auto kern, uint32_t pass, uint32_t per_cu) {
+    auto run = [&](auto kern, uint32_t pass, uint32_t per_cu, uint32_t nt = 256u) {
         DecParams Q = P;
         Q.pass = pass;
         const dim3 gq(pass <= 1 ? P.n_blocks : std::min<uint32_t>(P.n_blocks, per_cu * cus));
-        hipLaunchKernelGGL(kern, gq, dim3(256), 0, stream, Q);
+        hipLaunchKernelGGL(kern, gq, dim3(nt), 0, stream, Q);
     };
+    // 2-state blocks with more than 256 segments (checkpoints every <= 64
+    // pairs at 64 KiB): 512-thread workgroups, one segment per thread -- the
+    // same LDS per block, twice the waves per CU
+    const uint32_t bs = P.block_size;
+    const uint32_t pm = bs < 2u ? 0u : (bs & 1u) ? (bs - 3u) / 2u : bs / 2u - 1u;  // main-loop pairs of a full block
+    const uint32_t nseg = pm / std::max(P.ckpt_interval, 1u) + 1u;
+    const bool wide = P.nstates == 2 && nseg > 256u;
     if (P.nstates == 1) {
         if (lmax <= 11) {
             run(decode_pre_kernel<11, PP, 1, 1>, 1, 0);
@@ -1511,9 +1519,15 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
             run(decode_pre_kernel<15, 16, 1, 0>, 0, 0);
         }
     } else {
-        if (lmax <= 11) {
+        if (lmax <= 11 && wide) {
+            run(decode_pre_kernel<11, PP, 2, 1, 512>, 1, 0, 512);
+            run(decode_pre_kernel<11, PB, 2, 2, 512>, 2, 2, 512);
+        } else if (lmax <= 11) {
             run(decode_pre_kernel<11, PP, 2, 1>, 1, 0);
             run(decode_pre_kernel<11, PB, 2, 2>, 2, 2);
+        } else if (lmax <= 12 && wide) {
+            run(decode_pre_kernel<12, PP - 8192, 2, 1, 512>, 1, 0, 512);
+            run(decode_pre_kernel<12, PB, 2, 2, 512>, 2, 2, 512);
         } else if (lmax <= 12) {
             run(decode_pre_kernel<12, PP - 8192, 2, 1>, 1, 0);
             run(decode_pre_kernel<12, PB, 2, 2>, 2, 2);
@@ -1536,6 +1550,7 @@ int occupancy_report_dec(char* buf, int cap) {
                             fa.numRegs);
     };
     one("decode_pre<11,45056,2,1>", reinterpret_cast<const void*>(decode_pre_kernel<11, 45056u, 2, 1>));
+    one("decode_pre<11,45056,2,1,512>", reinterpret_cast<const void*>(decode_pre_kernel<11, 45056u, 2, 1, 512>));
     one("decode_pre<11,67584,2,2>", reinterpret_cast<const void*>(decode_pre_kernel<11, 67584u, 2, 2>));
     return len;
 }

@@ -159,12 +159,22 @@ struct Emit {
 // the 16 lanes of each dwordx4 read group on distinct 16-byte bank slots.
 constexpr uint32_t RING_STRIDE = 20;
 
+// A lane's checkpoints (its range holds at most S / interval of them) are
+// kept in registers and written together after its emit pass: recorded one
+// by one, 8-byte stores from 64 lanes at a 32-byte stride hit every 128-byte
+// line of the sidecar at four different times, and the lines left L2 part
+// written (sidecar WRITE_SIZE 3.8x its bytes at C2).
+constexpr uint32_t CKQ = 8;
 struct Ckpt {
     uint64_t* base;  // this block's sidecar entries, or nullptr
     uint32_t mask;   // interval - 1 (interval is a power of two, >= 8)
     uint32_t shift;  // log2(interval)
     uint32_t hdr_bits;
     uint32_t L;
+    bool queue;       // buffer this lane's entries (<= CKQ of them)
+    uint32_t cnt;     // entries buffered
+    uint32_t lo;      // index of q[0]
+    uint64_t q[CKQ];  // q[0] = the latest entry (lowest index)
 };
 
 enum { PASS_COUNT = 1, PASS_EMIT = 2, PASS_REPAIR = 3 };
@@ -262,9 +272,29 @@ __device__ __forceinline__ void enc_chunk(const uint4& q, uint32_t c8, uint32_t 
 // encoding pair p): bit position (payload-relative) and both states.
 // (NS = 1: one state, s1 = 0.)
 template <int NS>
-__device__ __forceinline__ void ckpt_record(const Ckpt& ck, uint32_t p, uint32_t pos, uint32_t x0, uint32_t x1) {
-    ck.base[p >> ck.shift] = (uint64_t)(pos - ck.hdr_bits) | ((uint64_t)(x0 - (1u << ck.L)) << 32) |
-                             (NS == 2 ? ((uint64_t)(x1 - (1u << ck.L)) << 48) : 0ull);
+__device__ __forceinline__ uint64_t ckpt_entry(const Ckpt& ck, uint32_t pos, uint32_t x0, uint32_t x1) {
+    return (uint64_t)(pos - ck.hdr_bits) | ((uint64_t)(x0 - (1u << ck.L)) << 32) |
+           (NS == 2 ? ((uint64_t)(x1 - (1u << ck.L)) << 48) : 0ull);
+}
+template <int NS>
+__device__ __forceinline__ void ckpt_record(Ckpt& ck, uint32_t p, uint32_t pos, uint32_t x0, uint32_t x1) {
+    const uint64_t e = ckpt_entry<NS>(ck, pos, x0, x1);
+    if (ck.queue) {  // block-uniform
+#pragma unroll
+        for (int i = (int)CKQ - 1; i > 0; --i) ck.q[i] = ck.q[i - 1];
+        ck.q[0] = e;
+        ck.lo = p >> ck.shift;
+        ++ck.cnt;
+    } else {
+        ck.base[p >> ck.shift] = e;
+    }
+}
+// The buffered entries, lowest index first: lane after lane, contiguous.
+__device__ __forceinline__ void ckpt_flush(const Ckpt& ck) {
+    if (!ck.queue) return;
+#pragma unroll
+    for (uint32_t i = 0; i < CKQ; ++i)
+        if (i < ck.cnt) ck.base[ck.lo + i] = ck.q[i];
 }
 
 // Encode pairs pb-1 down to pa.  Source chunks (16 B = 8 pairs) stream
@@ -274,7 +304,7 @@ __device__ __forceinline__ void ckpt_record(const Ckpt& ck, uint32_t p, uint32_t
 // segment); the partial topmost chunk is peeled and loaded byte-wise.
 template <int MODE, int NS>
 __device__ __forceinline__ EncState enc_range(const uint8_t* __restrict__ blk, uint32_t n, uint32_t pa, uint32_t pb,
-                                              EncState st, const EncTab& T, Emit& em, const Ckpt& ck, Track& tr) {
+                                              EncState st, const EncTab& T, Emit& em, Ckpt& ck, Track& tr) {
     constexpr bool TRACK = MODE == PASS_COUNT || MODE == PASS_REPAIR;
     uint32_t x0 = st.x0, x1 = st.x1, bits = st.bits;
     if (pb <= pa) return st;
@@ -571,7 +601,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     const uint32_t pa = k * S, pb = min(pa + S, Pm);
     Emit em;
     em.start(nullptr, 0);
-    Ckpt ck{nullptr, 0, 0, 0, L};
+    Ckpt ck{nullptr, 0, 0, 0, L, false, 0, 0, {}};
 
     // Exact start state of every lane (the lane above's end state) and
     // exact bit offset of every lane: count pass from guessed starts with
@@ -655,16 +685,18 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
                 ck.mask = P.ckpt_interval - 1u;
                 ck.shift = 31u - __clz(P.ckpt_interval);
                 ck.hdr_bits = hdr_bits;
+                ck.queue = ((S + ck.mask) >> ck.shift) <= CKQ;  // entries in [pa, pa + S)
             }
             EncState e0;
             if (k == ktop) {
                 e0 = top_start<PASS_EMIT, NS>(blk, n, tab, em);
-                if (ck.base && (Pm & ck.mask) == 0u)  // checkpoint "before step Pm"
-                    ckpt_record<NS>(ck, Pm, em.pos(), e0.x0, e0.x1);
+                if (ck.base && (Pm & ck.mask) == 0u)  // checkpoint "before step Pm" (outside [pa, pb))
+                    ck.base[Pm >> ck.shift] = ckpt_entry<NS>(ck, em.pos(), e0.x0, e0.x1);
             } else {
                 e0 = EncState{start & 0xFFFFu, start >> 16, 0u};
             }
             e0 = enc_range<PASS_EMIT, NS>(blk, n, pa, pb, e0, tab, em, ck, tr);
+            ckpt_flush(ck);
             const uint32_t y0 = e0.x0, y1 = e0.x1;
             if (k == 0) {  // Encoder::finish (x2 for NS = 2) + marker (lib.rs:178-181 / 139-141)
                 const uint32_t m = (1u << L) - 1u;

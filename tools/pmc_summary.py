@@ -29,8 +29,8 @@ def classify(kernel: str, groups: int, nth: int = 0):
     if "dtable_blocks_kernel" in kernel:
         return "fse_build_dtables" + ("_c3" if c3 else "")
     if "decode_pre_kernel" in kernel:
-        if "67584u" in kernel:
-            return "fse_decode_deferred" + ("_c3" if c3 else "")
+        if "67584u" in kernel:  # the list pass: a fixed grid, C2 launches first (twice), then C3
+            return "fse_decode_deferred" + ("_c3" if nth >= 2 else "")
         return "fse_decode_blocks" + ("_c3" if c3 else "")
     for k, name in (("serial_ring_kernel", "fse_decode_serial"), ("serial2_decode_kernel", "fse_decode_serial2"), ("decode_blocks_kernel", "fse_decode_fused"),
                     ("decode1_serial_kernel", "fse_decode1_serial"), ("pack_blocks_kernel", "fse_pack_blocks"),
