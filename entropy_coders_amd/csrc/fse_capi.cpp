@@ -169,11 +169,11 @@ uint32_t lmax_for(const fsehip_params* p) {
 }
 
 // Kernel table bound for a max_table_log: tables are instantiated at 11
-// (L <= 11), 12 and 15 (L 13..15; normalize clamps requests to 15,
+// (L <= 11), 12, 13, 14 and 15 (normalize clamps requests to 15,
 // histogram.rs:96); 0 = 12.  Decode tables use this stride.
 uint32_t kern_lmax(uint32_t max_table_log) {
     if (max_table_log == 0) return 12;
-    return max_table_log <= 11 ? 11 : max_table_log <= 12 ? 12 : 15;
+    return max_table_log <= 11 ? 11 : max_table_log >= 15 ? 15 : max_table_log;
 }
 
 // Device staging for the host-pointer entry points (grow-only, per thread).

@@ -1473,11 +1473,15 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
         if (P.nstates == 1) {
             if (lmax <= 11) hipLaunchKernelGGL((serial_ring_kernel<11, 6, 1>), dim3((P.n_blocks + 5u) / 6u), dim3(128), 0, stream, P);
             else if (lmax <= 12) hipLaunchKernelGGL((serial_ring_kernel<12, 3, 1>), dim3((P.n_blocks + 2u) / 3u), dim3(128), 0, stream, P);
+            else if (lmax <= 13) hipLaunchKernelGGL((decode1_serial_kernel<13>), g, dim3(64), 0, stream, P);
+            else if (lmax <= 14) hipLaunchKernelGGL((decode1_serial_kernel<14>), g, dim3(64), 0, stream, P);
             else hipLaunchKernelGGL((decode1_serial_kernel<15>), g, dim3(64), 0, stream, P);
         } else {
             // 6 (L <= 11) or 3 (L = 12) blocks per workgroup: 24 / 12 chains per CU (LDS-bound)
             if (lmax <= 11) hipLaunchKernelGGL((serial_ring_kernel<11, 6, 2>), dim3((P.n_blocks + 5u) / 6u), dim3(128), 0, stream, P);
             else if (lmax <= 12) hipLaunchKernelGGL((serial_ring_kernel<12, 3, 2>), dim3((P.n_blocks + 2u) / 3u), dim3(128), 0, stream, P);
+            else if (lmax <= 13) hipLaunchKernelGGL((serial2_decode_kernel<13>), g, dim3(64), 0, stream, P);
+            else if (lmax <= 14) hipLaunchKernelGGL((serial2_decode_kernel<14>), g, dim3(64), 0, stream, P);
             else hipLaunchKernelGGL((serial2_decode_kernel<15>), g, dim3(64), 0, stream, P);
         }
         return hipGetLastError();
@@ -1515,6 +1519,10 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
         } else if (lmax <= 12) {
             run(decode_pre_kernel<12, PP - 8192, 1, 1>, 1, 0);
             run(decode_pre_kernel<12, PB, 1, 2>, 2, 2);
+        } else if (lmax <= 13) {
+            run(decode_pre_kernel<13, 16, 1, 0>, 0, 0);
+        } else if (lmax <= 14) {
+            run(decode_pre_kernel<14, 16, 1, 0>, 0, 0);
         } else {
             run(decode_pre_kernel<15, 16, 1, 0>, 0, 0);
         }
@@ -1531,6 +1539,10 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
         } else if (lmax <= 12) {
             run(decode_pre_kernel<12, PP - 8192, 2, 1>, 1, 0);
             run(decode_pre_kernel<12, PB, 2, 2>, 2, 2);
+        } else if (lmax <= 13) {
+            run(decode_pre_kernel<13, 16, 2, 0>, 0, 0);
+        } else if (lmax <= 14) {
+            run(decode_pre_kernel<14, 16, 2, 0>, 0, 0);
         } else {
             run(decode_pre_kernel<15, 16, 2, 0>, 0, 0);
         }
@@ -1559,6 +1571,8 @@ hipError_t launch_dtables(const DtParams& P, uint32_t lmax, hipStream_t stream) 
     const dim3 g(P.n_blocks), b(64);
     if (lmax <= 11) hipLaunchKernelGGL((dtable_blocks_kernel<11>), g, b, P.xlds, stream, P);
     else if (lmax <= 12) hipLaunchKernelGGL((dtable_blocks_kernel<12>), g, b, P.xlds, stream, P);
+    else if (lmax <= 13) hipLaunchKernelGGL((dtable_blocks_kernel<13>), g, b, P.xlds, stream, P);
+    else if (lmax <= 14) hipLaunchKernelGGL((dtable_blocks_kernel<14>), g, b, P.xlds, stream, P);
     else hipLaunchKernelGGL((dtable_blocks_kernel<15>), g, b, P.xlds, stream, P);
     return hipGetLastError();
 }

@@ -918,6 +918,8 @@ hipError_t launch_encode(const EncParams& P, uint32_t lmax, hipStream_t stream) 
     if (P.nstates == 1) {  // fse_compress (lib.rs:112-143)
         if (lmax <= 11) go(encode_blocks_kernel<11, 64, 1>);
         else if (lmax <= 12) go(encode_blocks_kernel<12, 64, 1>);
+        else if (lmax <= 13) go(encode_blocks_kernel<13, 64, 1>);
+        else if (lmax <= 14) go(encode_blocks_kernel<14, 64, 1>);
         else go(encode_blocks_kernel<15, 64, 1>);
     } else if (T == 64) {
         // 11 workgroups per CU rather than the 12 its 12.6 KB allow: same
@@ -933,6 +935,8 @@ hipError_t launch_encode(const EncParams& P, uint32_t lmax, hipStream_t stream) 
         }();
         if (lmax <= 11) go(encode_blocks_kernel<11, 64, 2>, pad11);
         else if (lmax <= 12) go(encode_blocks_kernel<12, 64, 2>);
+        else if (lmax <= 13) go(encode_blocks_kernel<13, 64, 2>);
+        else if (lmax <= 14) go(encode_blocks_kernel<14, 64, 2>);
         else go(encode_blocks_kernel<15, 64, 2>);
     } else {
         if (lmax <= 11) go(encode_blocks_kernel<11, 32, 2>);

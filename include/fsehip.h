@@ -299,8 +299,8 @@ int fsehip_decompress_blocks(const fsehip_params* p, const uint8_t* d_in, uint64
 /* Decode tables, built once per block (NormHistogram::read + DecodeTable,
  * histogram.rs:436-505, fse.rs:280-338) for decode-only workloads (C3):
  * d_dtables holds fsehip_dtable_bytes(max_table_log) bytes per block (entry
- * u32 = nbBits | symbol << 8 | newState << 18 for max_table_log <= 12, and
- * newState << 17 above), d_dtinfo one int32 per
+ * u32 = nbBits | symbol << 8 | newState << 18 for max_table_log <= 14, and
+ * newState << 17 at 15), d_dtinfo one int32 per
  * block (header bytes | tableLog << 16, or a negative status). */
 uint64_t fsehip_dtable_bytes(uint32_t max_table_log);
 int fsehip_build_dtables(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
@@ -330,10 +330,9 @@ int fsehip_build_sidecar(const fsehip_params* p, const uint8_t* d_in, uint64_t s
  * d_status[b]: DST_TOO_SMALL when out_stride is short, SINGLE_SYMBOL for a
  * stream the crate would decode forever, UNSUPPORTED for a table log above
  * the kernels' bound or a stream above 2^28 bytes.  The bound is
- * max_table_log rounded up to a kernel variant: 11 (0 = 11), 12, or 15 for
- * 13..15 -- so max_table_log 13 or 14 accepts every stream, on the slower
- * global-memory kernels; the decode-table workspace is 4 << bound bytes per
- * stream (8 KiB at 11, 16 KiB at 12, 128 KiB at 15).
+ * max_table_log (0 = 11; below 11 it is 11: the smallest kernel variant);
+ * the decode-table workspace is 4 << bound bytes per stream (8 KiB at 11,
+ * 16 KiB at 12, 32 / 64 / 128 KiB at 13 / 14 / 15).
  * out_stride must be a multiple of 16 and d_out 16-byte aligned (the decoder
  * stores 16-byte groups; BAD_ARG otherwise).
  * Serial per stream, many streams at once. */
