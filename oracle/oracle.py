@@ -275,19 +275,25 @@ def bits_read_stack(data, widths) -> tuple[list[int], int]:
     return [int(x) for x in out], left.value
 
 
-def compress2_blocks(src: np.ndarray, block: int, threads: int):
+def compress2_blocks(src: np.ndarray, block: int, threads: int, dst: np.ndarray = None, lens: np.ndarray = None):
+    """`dst` / `lens`: reused output buffers (already faulted in), or None."""
     n_blocks = (len(src) + block - 1) // block
     slot = compress_bound(block)
-    dst = np.empty(n_blocks * slot, dtype=np.uint8)
-    lens = np.zeros(n_blocks, dtype=np.uint32)
+    if dst is None:
+        dst = np.empty(n_blocks * slot, dtype=np.uint8)
+    if lens is None:
+        lens = np.zeros(n_blocks, dtype=np.uint32)
+    assert len(dst) >= n_blocks * slot and len(lens) >= n_blocks
     _check(lib().fo_compress2_blocks(_ptr(src), len(src), block, _ptr(dst), slot, _ptr(lens),
                                      threads))
     return dst, lens, slot
 
 
 def decompress2_blocks(comp: np.ndarray, slot: int, lens: np.ndarray, block: int, n_total: int,
-                       threads: int) -> np.ndarray:
-    out = np.empty(n_total, dtype=np.uint8)
+                       threads: int, out: np.ndarray = None) -> np.ndarray:
+    if out is None:
+        out = np.empty(n_total, dtype=np.uint8)
+    assert len(out) >= n_total
     _check(lib().fo_decompress2_blocks(_ptr(comp), slot, _ptr(lens), len(lens), _ptr(out), block,
                                        n_total, threads))
     return out
