@@ -97,3 +97,27 @@ def test_deferred_pass_many_blocks(torch_cuda):
     lens = _check(torch_cuda, codec, src, 3)
     assert np.count_nonzero(lens > 44 << 10) == 560
     assert np.count_nonzero((lens > MID[0]) & (lens <= MID[1])) == 140
+
+
+@pytest.mark.parametrize("ckpt", [64, 32])
+def test_wide_workgroups_fine_checkpoints(torch_cuda, ckpt):
+    """More than 256 segments per block (64 KiB blocks, checkpoints every 64
+    or 32 pairs): the segment decoder runs 512-thread workgroups, one segment
+    per thread at 64, two interleaved per thread at 32, on both stages; every
+    route must give the source back and the sidecar must be the oracle's."""
+    from entropy_coders_amd import BlockCodec
+
+    codec = BlockCodec(block_size=65536, ckpt_interval=ckpt)
+    src = _mixed_src(torch_cuda, codec, LAYOUT * 2)
+    _check(torch_cuda, codec, src, 4)
+    cb = codec.compress(src)
+    host = src.cpu().numpy()
+    side = cb["sidecar"].cpu().numpy().view(np.uint64)
+    per = codec.side_per_block
+    for b in (0, 2, 4):  # uniform, C2, p = 0.1
+        comp, _ = O.compress2(host[b * 65536:(b + 1) * 65536])
+        bp, s0, s1 = O.checkpoints2(comp, ckpt)
+        got = side[b * per: b * per + len(bp)]
+        assert np.array_equal(got & 0xFFFFFFFF, bp.astype(np.uint64)), b
+        assert np.array_equal((got >> 32) & 0xFFFF, s0.astype(np.uint64)), b
+        assert np.array_equal(got >> 48, s1.astype(np.uint64)), b
