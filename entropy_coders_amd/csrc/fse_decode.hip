@@ -331,11 +331,23 @@ __device__ __forceinline__ void run_groups_tx(Chain& c, uint32_t my_ng, uint32_t
             for (uint32_t j = 0; j < DEC_GROUP / 2u; ++j) w[j] = 0;
         }
         rows_transpose(w);
+#if FSEHIP_ABL & 16  // ablation (timing only): no output stores, the values kept live
+        (void)obase;
+        (void)ong;
+        (void)row;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            asm volatile("; sink %0 %1 %2 %3" ::"v"(w[4 * k]), "v"(w[4 * k + 1]), "v"(w[4 * k + 2]), "v"(w[4 * k + 3]));
+#else
+        // non-temporal: the output is written once and not read back here, so
+        // it should not displace the images, tables and sidecars in L2
+        // (C3 0.95 -> 0.91 ms, C2 decode 0.60 -> 0.57 ms, same box)
 #pragma unroll
         for (int k = 0; k < 4; ++k)
             if (g < ong[k])
-                *reinterpret_cast<uint4*>(obase[k] + g * 2u * DEC_GROUP + 16u * row) =
-                    make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+                __builtin_nontemporal_store(u32x4{w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]},
+                                            reinterpret_cast<u32x4*>(obase[k] + g * 2u * DEC_GROUP + 16u * row));
+#endif
     }
 }
 
