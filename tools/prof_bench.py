@@ -18,7 +18,8 @@ import torch  # noqa: E402
 
 from entropy_coders_amd import BlockCodec  # noqa: E402
 
-codec = BlockCodec(nstates=int(os.environ.get("PROF_NSTATES", 2)))
+# the bench's checkpoint interval (bench.py --ckpt default)
+codec = BlockCodec(nstates=int(os.environ.get("PROF_NSTATES", 2)), ckpt_interval=int(os.environ.get("PROF_CKPT", 64)))
 n = 1 << 30
 src = codec.generate(0, 0.155, 0x5EED0002, n)
 cb = codec.alloc(n)

@@ -26,7 +26,7 @@ def timed(fn, reps):
 
 reps = int(os.environ.get("REPS", 10))
 blocks = int(os.environ.get("C3_BLOCKS", 32768))
-ckpt = int(os.environ.get("CKPT", 128))
+ckpt = int(os.environ.get("CKPT", 64))
 codec = BlockCodec(block_size=65536, ckpt_interval=ckpt)
 n = blocks * 65536
 src = codec.generate(0, 0.155, 0x5EED0003, n)
