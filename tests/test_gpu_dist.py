@@ -25,10 +25,15 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, scheme, q):
+def _worker(rank, world, port, scheme, q, backend="gloo"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda:0"))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    host_t = (lambda t: t.cpu()) if backend == "gloo" else (lambda t: t)  # RCCL moves device tensors
     ok = False
     try:
         from entropy_coders_amd import BlockCodec
@@ -48,17 +53,17 @@ def _worker(rank, world, port, scheme, q):
         nb = len(mine)
         side = cb["sidecar"][: nb * codec.side_per_block]
         packed, _ = pack_device(cb["out"], codec.slot_bytes, cb["comp_len"])
-        streams, lens, sides = gather_stream(packed.cpu(), cb["comp_len"].cpu(), dst=0, sidecar=side.cpu())
+        streams, lens, sides = gather_stream(host_t(packed), host_t(cb["comp_len"]), dst=0, sidecar=host_t(side))
         g_stream = g_lens = g_side = None
         if rank == 0:
             host = raw.cpu().numpy()
             for b, (r, off, ln) in enumerate(assemble(streams, lens, NB, world, scheme)):
                 want = O.compress2(host[b * BS: min((b + 1) * BS, n_glob)])[0]
-                ok &= streams[r][off: off + ln].numpy().tobytes() == want
+                ok &= streams[r][off: off + ln].cpu().numpy().tobytes() == want
             g_stream, g_lens, g_side = concat_global(streams, lens, NB, world, scheme, sides)
         my, my_lens, my_side, idx = scatter_stream(g_stream, g_lens, src=0, sidecar=g_side,
                                                    side_per_block=codec.side_per_block, scheme=scheme,
-                                                   device="cpu")
+                                                   device="cpu" if backend == "gloo" else None)
         ok &= list(idx) == mine
         slots = unpack_device(my.cuda(), my_lens.cuda(), codec.slot_bytes)
         cb2 = {"n_total": local.numel(), "out": slots, "comp_len": my_lens.cuda(), "sidecar": my_side.cuda()}
@@ -72,13 +77,13 @@ def _worker(rank, world, port, scheme, q):
         if rank == 0 and scheme == "round_robin":
             from entropy_coders_amd.dist import exclusive_offsets, select_blocks
 
-            offs = exclusive_offsets(g_lens)
+            offs = exclusive_offsets(g_lens.cpu())
             sel = [9, 0, 4, 7, 1]
             dsel = select_blocks(g_stream.cuda(), offs.cuda(), g_lens.cuda(), sel)
-            hsel = select_blocks(g_stream, offs, g_lens, sel)
+            hsel = select_blocks(g_stream.cpu(), offs, g_lens.cpu(), sel)
             ok &= bool(torch.equal(dsel.cpu(), hsel))
     finally:
-        flag = torch.tensor([1 if ok else 0])
+        flag = torch.tensor([1 if ok else 0], device="cpu" if backend == "gloo" else "cuda:0")
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         if rank == 0:
             q.put(bool(flag.item()))
@@ -100,4 +105,23 @@ def test_two_ranks_encode_gather_scatter_decode(scheme):
         if p.exitcode is None:
             p.kill()
     assert codes == [0, 0], codes
+    assert q.get(timeout=10) is True
+
+
+@pytest.mark.parametrize("scheme", ["contiguous", "round_robin"])
+def test_rccl_one_rank_encode_gather_scatter_decode(scheme):
+    """The RCCL ("nccl") branch of dist.py on hardware: one rank (RCCL
+    needs a GPU per rank), device tensors through all_gather, broadcast
+    and the scatter's device-side block selection, bytes checked against
+    the oracle.  The N-rank p2p transfers run in the driver's multi-GPU
+    bench and in the gloo tests above."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker, args=(0, 1, _free_port(), scheme, q, "nccl"))
+    p.start()
+    p.join(110)
+    code = p.exitcode
+    if code is None:
+        p.kill()
+    assert code == 0, code
     assert q.get(timeout=10) is True
