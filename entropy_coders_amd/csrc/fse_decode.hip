@@ -564,7 +564,7 @@ __device__ __forceinline__ void decode_pre_block(const DecParams& P, Smem& sm, c
     const uint32_t* gw = reinterpret_cast<const uint32_t*>(in);
     int32_t err = FSE_OK;
     uint32_t base0 = 0;
-    if (NS == 2 && !BIG && in_lds) {
+    if (NS == 2 && !BIG && in_lds && NT <= 256u) {  // (512 lanes: one segment each per round, 64 VGPRs)
         // Two segments per lane while a round has more segments than lanes
         // (checkpoints every <= 64 pairs at 64 KiB): segments s and s + NT
         // decoded interleaved, two independent chains per lane.
