@@ -15,10 +15,11 @@
 //                          block with its table in LDS; can record the sidecar
 //   decode1_serial_kernel  the same for 1-state blocks (fse_decompress)
 //
-// Table logs: kernels are instantiated at LMAX = 11, 12 and 15 (blocks of
-// L 5..11, 12, 13..15).  At LMAX = 15 the table (128 KiB) leaves no LDS for
-// the block image, so those blocks are read through a register window from
-// global memory.
+// Table logs: kernels are instantiated at LMAX = 11, 12, 13, 14 and 15.  Up
+// to L = 14 the segment decoder stages the block image beside the table (32
+// and 64 KiB tables at 13 and 14: 2 and 1 workgroups per CU); at LMAX = 15
+// the table (128 KiB) leaves no LDS for the image, so those blocks are read
+// through a register window from global memory.
 #include <type_traits>
 
 #include "fse_device.hpp"
@@ -477,7 +478,7 @@ __device__ __forceinline__ int32_t run_chain1(LdsChain1& c, const uint32_t* pay,
 //   3. every segment's end is checked against the next checkpoint.
 // Blocks above the PMAX-byte stage are deferred (pass 1: status
 // FSE_DEFERRED) to a second launch with a 66 KiB stage (pass 2); at
-// LMAX > 12 the table alone fills the LDS and every block reads its payload
+// LMAX = 15 the table alone fills the LDS and every block reads its payload
 // through a global-memory window (pass 0).
 // ------------------------------------------------------------------------
 // Segment of thread tid in a round of 256.
@@ -506,7 +507,7 @@ struct PreSmem {
 // the next call's staging writes them.
 template <int LMAX, uint32_t PMAX, int NS, uint32_t NT, class Smem>
 __device__ __forceinline__ void decode_pre_block(const DecParams& P, Smem& sm, const uint64_t gb) {
-    constexpr bool BIG = LMAX > 12;  // no LDS image
+    constexpr bool BIG = LMAX > 14;  // no LDS image
     constexpr uint32_t NW = NT / 64u;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     if (gb >= P.n_blocks) return;
@@ -714,7 +715,7 @@ __device__ __forceinline__ void decode_pre_block(const DecParams& P, Smem& sm, c
 // per GiB).
 template <int LMAX, uint32_t PMAX, int NS, int PASS, uint32_t NT = 256u>
 __global__ __launch_bounds__(NT) void decode_pre_kernel(DecParams P) {
-    constexpr bool BIG = LMAX > 12;
+    constexpr bool BIG = LMAX > 14;
     constexpr uint32_t NW = NT / 64u;
     __shared__ PreSmem<LMAX, BIG ? 16u : PMAX, NW> sm;
     if constexpr (PASS <= 1) {
@@ -1537,9 +1538,11 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
             run(decode_pre_kernel<12, PP - 8192, 1, 1>, 1, 0);
             run(decode_pre_kernel<12, PB, 1, 2>, 2, 2);
         } else if (lmax <= 13) {
-            run(decode_pre_kernel<13, 16, 1, 0>, 0, 0);
+            run(decode_pre_kernel<13, PP, 1, 1>, 1, 0);
+            run(decode_pre_kernel<13, PB, 1, 2>, 2, 1);
         } else if (lmax <= 14) {
-            run(decode_pre_kernel<14, 16, 1, 0>, 0, 0);
+            run(decode_pre_kernel<14, PP, 1, 1>, 1, 0);
+            run(decode_pre_kernel<14, PB, 1, 2>, 2, 1);
         } else {
             run(decode_pre_kernel<15, 16, 1, 0>, 0, 0);
         }
@@ -1556,10 +1559,18 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
         } else if (lmax <= 12) {
             run(decode_pre_kernel<12, PP - 8192, 2, 1>, 1, 0);
             run(decode_pre_kernel<12, PB, 2, 2>, 2, 2);
+        } else if (lmax <= 13 && wide) {  // 32 KiB table: 2 workgroups per CU, the list pass 1
+            run(decode_pre_kernel<13, PP, 2, 1, 512>, 1, 0, 512);
+            run(decode_pre_kernel<13, PB, 2, 2, 512>, 2, 1, 512);
         } else if (lmax <= 13) {
-            run(decode_pre_kernel<13, 16, 2, 0>, 0, 0);
+            run(decode_pre_kernel<13, PP, 2, 1>, 1, 0);
+            run(decode_pre_kernel<13, PB, 2, 2>, 2, 1);
+        } else if (lmax <= 14 && wide) {  // 64 KiB table: 1 workgroup per CU
+            run(decode_pre_kernel<14, PP, 2, 1, 512>, 1, 0, 512);
+            run(decode_pre_kernel<14, PB, 2, 2, 512>, 2, 1, 512);
         } else if (lmax <= 14) {
-            run(decode_pre_kernel<14, 16, 2, 0>, 0, 0);
+            run(decode_pre_kernel<14, PP, 2, 1>, 1, 0);
+            run(decode_pre_kernel<14, PB, 2, 2>, 2, 1);
         } else {
             run(decode_pre_kernel<15, 16, 2, 0>, 0, 0);
         }

@@ -375,3 +375,35 @@ def test_workspace_shared_stream_two_threads(torch_cuda):
     for t in th:
         t.join()
     assert not errors, errors
+
+
+@pytest.mark.parametrize("nstates,ckpt", [(2, 128), (2, 64), (1, 64)])
+@pytest.mark.parametrize("L", [13, 14])
+def test_lds_stage_decode_table_logs_13_14(torch_cuda, L, nstates, ckpt):
+    """Table logs 13 and 14 decode through the LDS-staged segment kernel (32 /
+    64 KiB tables beside the block image): skewed blocks in the 44 KiB stage,
+    near-uniform ones (~65 KB) deferred to the 66 KiB list pass, mixed in one
+    batch.  Sampled blocks equal the oracle's bytes; every block decodes
+    back to its source, with and without the sidecar."""
+    torch = torch_cuda
+    from entropy_coders_amd import BlockCodec
+
+    B = 65536
+    codec = BlockCodec(block_size=B, table_log=L, ckpt_interval=ckpt, nstates=nstates)
+    kinds = [(0, 0.77), (2, 0.0), (0, 0.155), (2, 0.0), (0, 0.77), (0, 0.155)]  # 2: near-uniform
+    src = torch.cat([codec.generate(k, p, 0x5EED00C0 + 7 * i + L, B) for i, (k, p) in enumerate(kinds)])
+    src = src[: len(kinds) * B - 333]  # a ragged last block
+    host = src.cpu().numpy()
+    cb = codec.compress(src)
+    torch.cuda.synchronize()
+    assert int(cb["status"].abs().max()) == 0, cb["status"].cpu().numpy()
+    for b in (0, 1, 5):  # (the reference's 1-state fse_compress has no table-log argument)
+        want = O.compress2(host[b * B:(b + 1) * B], L)[0] if nstates == 2 else O.compress(host[b * B:(b + 1) * B])[0]
+        if nstates == 2:
+            assert codec.block_bytes(cb, b) == want, b
+    lens = cb["comp_len"].cpu().numpy()
+    assert lens.max() > 44 * 1024 and lens.min() < 44 * 1024  # both passes run
+    for side in (True, False):
+        out, st = codec.decompress(cb, use_sidecar=side)
+        torch.cuda.synchronize()
+        assert int(st.abs().max()) == 0 and torch.equal(out, src), side
