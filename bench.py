@@ -60,6 +60,7 @@ def parse():
     ap.add_argument("--c3-blocks", type=int, default=32768,
                     help="C3 size: blocks of C2 data (32768 x 64 KiB ~ 1 GiB compressed, SURVEY 8(d))")
     ap.add_argument("--no-serial", action="store_true", help="skip the sidecar-less decode line")
+    ap.add_argument("--no-onestate", action="store_true", help="skip the 1-state format line")
     ap.add_argument("--no-sweep", action="store_true", help="skip the C5 distribution / table-log sweep")
     ap.add_argument("--sweep-bytes", type=int, default=256 << 20, help="raw bytes per C5 sweep point")
     ap.add_argument("--host", action="store_true",
@@ -503,6 +504,44 @@ def main():
         ok = ok and c3_ok
         del src3, cb3, tabs, out3, st3
 
+    # the same 1 GiB in the 1-state format (fse_compress blocks,
+    # lib.rs:112-141 / 187-211), encode + decode with its sidecar, verified
+    one_state = None
+    if not args.no_onestate and world == 1 and args.nstates == 2:
+        # checkpoints every 2 x ckpt symbols (the 2-state step's segment length in symbols: one
+        # segment per thread of the 512-thread workgroups; 1,057-1,061 vs 1,013-1,020 GiB/s
+        # decode at 4 x ckpt, same box)
+        c1 = BlockCodec(block_size=args.block, ckpt_interval=int(os.environ.get("FSEHIP_CKPT1", 2 * args.ckpt)),
+                        device=dev, nstates=1)
+        cb1 = c1.alloc(n)
+        out1 = torch.empty(n, dtype=torch.uint8, device=dev)
+        st1 = torch.zeros(c1.n_blocks(n), dtype=torch.int32, device=dev)
+        c1.compress_into(src, cb1)  # warm-up
+        c1.decompress_into(cb1, out1, st1)
+        out1.fill_(0xA5)
+        st1.fill_(-99)
+        torch.cuda.synchronize(dev)
+        e1 = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        reps = 3
+        e1[0].record(stream)
+        for _ in range(reps):
+            c1.compress_into(src, cb1)
+        e1[1].record(stream)
+        for _ in range(reps):
+            c1.decompress_into(cb1, out1, st1)
+        e1[2].record(stream)
+        torch.cuda.synchronize(dev)
+        enc1, dec1 = e1[0].elapsed_time(e1[1]) / reps, e1[1].elapsed_time(e1[2]) / reps
+        ok1 = int(cb1["status"].abs().max()) == 0 and int(st1.abs().max()) == 0 and bool(torch.equal(out1, src))
+        one_state = {"workload": "the step's 1 GiB as 1-state blocks (fse_compress), encode + decode with the "
+                                 f"sidecar ({c1.ckpt_interval}-symbol checkpoints), HIP events",
+                     "compressed_ratio": round(int(cb1["comp_len"].to(torch.int64).sum()) / n, 5),
+                     "encode_GiB_s": round(n / (enc1 * 1e-3) / 2**30, 2),
+                     "decode_GiB_s": round(n / (dec1 * 1e-3) / 2**30, 2),
+                     "roundtrip_GiB_s": round(n / ((enc1 + dec1) * 1e-3) / 2**30, 2), "verified": ok1}
+        ok = ok and ok1
+        del c1, cb1, out1, st1
+
     host_info = None
     if args.host and world == 1:
         from entropy_coders_amd.stream import HostPipeline
@@ -571,6 +610,8 @@ def main():
             line["c3_decode_only"] = c3
         if serial is not None:
             line["sidecar_less_decode"] = serial
+        if one_state is not None:
+            line["one_state"] = one_state
         if gather_info is not None:
             line["c4_exchange"] = gather_info
         if host_info is not None:

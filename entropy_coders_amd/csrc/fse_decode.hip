@@ -1523,15 +1523,19 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
         const dim3 gq(pass <= 1 ? P.n_blocks : std::min<uint32_t>(P.n_blocks, per_cu * cus));
         hipLaunchKernelGGL(kern, gq, dim3(nt), 0, stream, Q);
     };
-    // 2-state blocks with more than 256 segments (checkpoints every <= 64
-    // pairs at 64 KiB): 512-thread workgroups, one segment per thread -- the
-    // same LDS per block, twice the waves per CU
+    // blocks with more than 256 segments (checkpoints every <= 64 pairs or
+    // 128 symbols at 64 KiB): 512-thread workgroups, one segment per thread --
+    // the same LDS per block, more waves per CU
     const uint32_t bs = P.block_size;
-    const uint32_t pm = bs < 2u ? 0u : (bs & 1u) ? (bs - 3u) / 2u : bs / 2u - 1u;  // main-loop pairs of a full block
+    // main-loop steps of a full block: pairs (2-state) or symbols (1-state)
+    const uint32_t pm = bs < 2u ? 0u : P.nstates == 1 ? bs - 1u : (bs & 1u) ? (bs - 3u) / 2u : bs / 2u - 1u;
     const uint32_t nseg = pm / std::max(P.ckpt_interval, 1u) + 1u;
-    const bool wide = P.nstates == 2 && nseg > 256u;
+    const bool wide = nseg > 256u;
     if (P.nstates == 1) {
-        if (lmax <= 11) {
+        if (lmax <= 11 && wide) {  // 1-state checkpoints every <= 128 symbols: one segment per thread of 512
+            run(decode_pre_kernel<11, PP, 1, 1, 512>, 1, 0, 512);
+            run(decode_pre_kernel<11, PB, 1, 2, 512>, 2, 2, 512);
+        } else if (lmax <= 11) {
             run(decode_pre_kernel<11, PP, 1, 1>, 1, 0);
             run(decode_pre_kernel<11, PB, 1, 2>, 2, 2);
         } else if (lmax <= 12) {
