@@ -154,7 +154,7 @@ struct Stamps {
         fprintf(stderr, "[stamps] %s counters: lo %.3f hi %.3f (mean per workgroup)\n", what, lo / groups, hi / groups);
     }
 };
-Stamps g_stamps_enc, g_stamps_dec;
+Stamps g_stamps_enc, g_stamps_dec, g_stamps_dt;
 
 bool device_ok() {
     int n = 0;
@@ -384,7 +384,9 @@ int fsehip_build_dtables(const fsehip_params* p, const uint8_t* d_in, uint64_t s
     D.dt = d_dtables;
     D.dtinfo = d_dtinfo;
     D.xlds = env_u32("FSEHIP_DT_XLDS", 0);  // diagnostics: occupancy probe
+    D.stamps = g_stamps_dt.get(n_blocks);
     hipError_t e = fsehip::launch_dtables(D, kern_lmax(p->max_table_log), static_cast<hipStream_t>(stream));
+    if (D.stamps) g_stamps_dt.report("dtables", n_blocks, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? FSE_OK : FSE_ERR_HIP;
 }
 

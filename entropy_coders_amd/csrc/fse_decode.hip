@@ -770,6 +770,7 @@ __global__ __launch_bounds__(64) void dtable_blocks_kernel(DtParams P) {
     const uint32_t lane = lane_id();
     const uint64_t gb = blockIdx.x;
     if (gb >= P.n_blocks) return;
+    FSE_STAMP(P, 0);
     const uint8_t* in = P.in + gb * P.slot_bytes;
     const uint32_t clen = P.comp_len[gb];
     const uint32_t* w = reinterpret_cast<const uint32_t*>(in);
@@ -793,7 +794,9 @@ __global__ __launch_bounds__(64) void dtable_blocks_kernel(DtParams P) {
     for (uint32_t s = lane; s < 256u; s += WAVE) norm[s] = 0;
     wave_sync();
     uint32_t L = 0, tl = 0;
+    FSE_STAMP(P, 1);
     const int hl = header_read_wave(r0, r1, clen, (uint32_t)LMAX, norm, &L, &tl);
+    FSE_STAMP(P, 2);
     int rc = hl < 0 ? hl : FSE_OK;
     if (rc == FSE_OK && ((uint32_t)hl >= clen || last == 0)) rc = FSE_ERR_NO_MARKER;  // lib.rs:222
     if (rc == FSE_OK && clen > (1u << 28)) rc = FSE_ERR_UNSUPPORTED;  // bit positions are 32-bit in the decoders
@@ -808,9 +811,10 @@ __global__ __launch_bounds__(64) void dtable_blocks_kernel(DtParams P) {
             dt[i] = Dte<LMAX>::make(nb, s, (nx << nb) - size);
         };
         // two-pass ranks need 2^L / 64 per-chunk registers: up to L = 12
-        if (LMAX <= 12) rc = wave_build_spread<SIZE / 64u>(norm, L, tl, sym_at, occ, cumul, cnt, visit, rk, pm);
+        if (LMAX <= 12) rc = wave_build_spread<SIZE / 64u>(norm, L, tl, sym_at, occ, cumul, cnt, visit, rk, pm, &P);
         else rc = wave_build_spread(norm, L, tl, sym_at, occ, cumul, cnt, visit);
     }
+    FSE_STAMP(P, 8);
     if (lane == 0) P.dtinfo[gb] = rc == FSE_OK ? (int32_t)((uint32_t)hl | (L << 16)) : rc;
 }
 

@@ -20,6 +20,10 @@ namespace fsehip {
             (P).stamps[(uint64_t)blockIdx.x * kStamps + (slot)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 
+#ifndef FSEHIP_KSTAMPS
+#define FSEHIP_KSTAMPS
+constexpr int kStamps = 10;  // stamp slots per workgroup (diagnostics; also in fse_kernels.h)
+#endif
 constexpr uint32_t LOG_MIN = 5;       // lib.rs:9
 constexpr uint32_t LOG_MAX_REF = 15;  // lib.rs:10
 constexpr uint32_t LOG_DEFAULT = 11;  // lib.rs:12
@@ -768,10 +772,18 @@ __device__ inline int header_read_wave(uint32_t r0, uint32_t r1, uint32_t n, uin
 // Exclusive scan helpers on DPP: wave_shr:1 (lane 0 reads 0).
 __device__ __forceinline__ uint32_t wave_shr1(uint32_t v) { return dpp0<0x138, 0xf>(v); }
 
-template <uint32_t MAXCH = 64, typename Visit>  // MAXCH: 2^LMAX / 64 chunks (two-pass ranks)
+struct NoStamps {
+    uint64_t* stamps = nullptr;
+};
+template <uint32_t MAXCH = 64, typename Visit, class SP = NoStamps>  // MAXCH: 2^LMAX / 64 chunks (two-pass ranks)
 __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_t tl, uint8_t* sym_at,
                                         uint8_t* occ_sym, uint16_t* cumul, uint32_t* cnt, Visit visit,
-                                        uint16_t* RK = nullptr, uint64_t* PM = nullptr) {
+                                        uint16_t* RK = nullptr, uint64_t* PM = nullptr, const SP* SPp = nullptr) {
+    // SPp: diagnostics only, a params struct with `stamps` (phase stamps 3..7)
+#define SPREAD_STAMP(k)                                  \
+    do {                                                 \
+        if (SPp) FSE_STAMP(*SPp, k);                     \
+    } while (0)
     const uint32_t lane = lane_id();
     const uint32_t size = 1u << L;
     const uint32_t mask = size - 1u;
@@ -796,6 +808,7 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
     const uint32_t total_pos = bcast63(ex_p + sum_p);
     if (total_pos + total_neg > size || total_neg > size) return FSE_ERR_BAD_TABLE;
     const int32_t ht = (int32_t)size - 1 - (int32_t)total_neg;
+    SPREAD_STAMP(3);
     for (uint32_t i = lane; i < size / 16u; i += WAVE) {  // size >= 32: whole 16-byte stores
         reinterpret_cast<uint4*>(occ_sym)[i] = make_uint4(0, 0, 0, 0);
         reinterpret_cast<uint4*>(sym_at)[i] = make_uint4(0, 0, 0, 0);
@@ -833,6 +846,7 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
         }
     }
     wave_sync();
+    SPREAD_STAMP(4);
     // spread: j-th valid multiplier -> position (multipliers 4q..4q+3 per lane)
     const uint32_t step = (size >> 3) * 5u + 3u;  // table_step: size*5/8+3 (fse.rs:67-70)
     {
@@ -859,6 +873,7 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
         if (j0 != total_pos) return FSE_ERR_BAD_TABLE;  // position != 0 assert
     }
     wave_sync();
+    SPREAD_STAMP(5);
     if (RK != nullptr && tl <= 64u && size >= WAVE) {
         // pass 1: per 64-position chunk t, each symbol's count at RK[t][s]
         // (written by its lowest lane) and each lane's peers below, packed
@@ -880,6 +895,7 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
             }
         }
         wave_sync();
+        SPREAD_STAMP(6);
         // per-symbol exclusive prefix over the chunks (lane = symbol)
         {
             uint32_t run = 0;
@@ -893,6 +909,7 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
             }
         }
         wave_sync();
+        SPREAD_STAMP(7);
         // pass 2: rank = the symbol's count in earlier chunks + peers below
 #pragma unroll
         for (uint32_t t = 0; t < MAXCH; ++t) {
@@ -924,6 +941,7 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
         wave_sync();
     }
     return FSE_OK;
+#undef SPREAD_STAMP
 }
 
 }  // namespace fsehip

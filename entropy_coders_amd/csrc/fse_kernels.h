@@ -62,6 +62,7 @@ struct DtParams {
     uint32_t* dt;      // [n_blocks][1 << lmax] entries (dte_make layout)
     int32_t* dtinfo;   // header bytes | L << 16, or < 0 = status
     uint32_t xlds;     // diagnostics: extra dynamic LDS bytes per workgroup (occupancy probe)
+    uint64_t* stamps;  // diagnostics: per-workgroup phase stamps (FSEHIP_STAMPS), or nullptr
 };
 
 struct GenParams {
@@ -102,7 +103,10 @@ hipError_t launch_bits_unpack(const uint8_t* in, uint64_t n_bytes, uint64_t tota
                               const uint8_t* nbits, const uint8_t* ops, uint64_t count, const uint64_t* tile_off,
                               const uint64_t* total, uint32_t* vals, uint64_t* result, hipStream_t s);
 
-constexpr int kStamps = 10;  // stamp slots per workgroup
+#ifndef FSEHIP_KSTAMPS
+#define FSEHIP_KSTAMPS
+constexpr int kStamps = 10;  // stamp slots per workgroup (also declared in fse_device.hpp)
+#endif
 constexpr int32_t FSE_DEFERRED = 1;  // internal block status between the decode passes
 
 hipError_t launch_encode(const EncParams& P, uint32_t lmax, hipStream_t stream);

@@ -14,7 +14,7 @@ n = 1 << 30
 codec = BlockCodec()
 src = codec.generate(0, 0.155, 0x5EED0002, n)
 cb = codec.compress(src)
-for wg in (20, 16, 20, 12, 10, 8, 20):
+for wg in [int(w) for w in os.environ.get("OCC_WGS", "20,16,20,12,10,8,20").split(",")]:
     x = max(0, LDS_CU // wg - BASE - 64) if wg < LDS_CU // BASE else 0
     os.environ["FSEHIP_DT_XLDS"] = str(x)
     t = timeit(lambda: codec.build_dtables(cb), reps=7)
