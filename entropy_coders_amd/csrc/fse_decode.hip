@@ -32,6 +32,9 @@
 #endif
 // cache policy of the segment decoder's LDS-DMA staging loads: nt (2), as the image and table
 // are read once (C3 0.96 -> 0.91-0.96 ms, C2 decode 0.558 -> 0.552-0.554 ms, same box)
+#ifndef FSEHIP_DEC1_TX  // 1-state segments through the transposed group stores
+#define FSEHIP_DEC1_TX 1
+#endif
 #ifndef FSEHIP_STAGE_AUX
 #define FSEHIP_STAGE_AUX 2
 #endif
@@ -440,6 +443,16 @@ struct LdsChain1 {
     }
 };
 
+// A 1-state chain as two steps per call (sym0 | sym1 << 8), for the
+// transposed group stores (run_groups_tx)
+struct Chain1x2 {
+    LdsChain1 c;
+    __device__ __forceinline__ uint32_t pair(const uint32_t* pay, const uint8_t* dtb) {
+        const uint32_t e0 = c.step(pay, dtb), e1 = c.step(pay, dtb);
+        return __builtin_amdgcn_perm(e1, e0, 0x0c0c0501u);
+    }
+};
+
 // Steps [p, p1) of one 1-state segment; the last segment then emits the
 // final state's symbol (container mode: the raw length ends the block, as
 // the reference's next read fails right there for a valid stream).
@@ -648,6 +661,50 @@ __device__ __forceinline__ void decode_pre_block(const DecParams& P, Smem& sm, c
             if (act) {
                 r = run_chain(c, sm.pay, dtb, p0 + my_ng * DEC_GROUP, p1, lastseg, n, Pm, out, hdr_bits);
                 if (r == FSE_OK && !lastseg && !ckpt_match(en, hdr_bits, smask, c.pos, c.s0() << 2, c.s1() << 2))
+                    r = FSE_ERR_BAD_SIDECAR;
+            }
+            if (r != FSE_OK) err = r;
+        }
+    }
+    if (NS == 1 && !BIG && in_lds && FSEHIP_DEC1_TX) {
+        // 1-state: the same transposed stores, 64 symbols (one 64-byte piece)
+        // per group, two chain steps per packed pair
+        constexpr uint32_t G1 = 2u * DEC_GROUP;
+        for (; base0 < nseg; base0 += NT) {
+            const uint32_t seg = base0 + seg_of<NT>(tid);
+            bool act = seg < nseg;
+            const uint32_t p0 = seg * I, p1 = act ? min(p0 + I, Pm) : p0;
+            const bool lastseg = seg == nseg - 1u;
+            int32_t r = FSE_OK;
+            Chain1x2 c;
+            uint64_t en = 0;
+            if (act) {
+                const uint64_t e = sc[seg];
+                en = lastseg ? 0ull : sc[seg + 1u];
+                if ((uint32_t)e > maxbp) {  // corrupt index: never read outside the block
+                    r = FSE_ERR_BAD_SIDECAR;
+                    act = false;
+                } else {
+                    c.c.init(sm.pay, hdr_bits + (int32_t)(uint32_t)e, (uint32_t)(e >> 32) & smask);
+                }
+            }
+            const uint32_t my_ng = act ? (p1 - p0) / G1 : 0u;
+            const uint32_t ng_max = wave_max(my_ng);
+            if (ng_max) {
+                uint8_t* obase[4];
+                uint32_t ong[4];
+#pragma unroll
+                for (uint32_t k = 0; k < 4; ++k) {
+                    const uint32_t os = base0 + seg_of<NT>((tid & ~63u) + 16u * k + (tid & 15u));
+                    const uint32_t oq = os * I;
+                    ong[k] = os < nseg ? (min(oq + I, Pm) - oq) / G1 : 0u;
+                    obase[k] = out + oq;
+                }
+                run_groups_tx(c, my_ng, ng_max, sm.pay, dtb, obase, ong, (tid >> 4) & 3u);
+            }
+            if (act) {
+                r = run_chain1(c.c, sm.pay, dtb, p0 + my_ng * G1, p1, lastseg, n, out, hdr_bits);
+                if (r == FSE_OK && !lastseg && !ckpt_match(en, hdr_bits, smask, c.c.pos, c.c.a, 0u))
                     r = FSE_ERR_BAD_SIDECAR;
             }
             if (r != FSE_OK) err = r;
