@@ -5,6 +5,8 @@ formats (fse_compress2 / fse_compress) and checkpoint intervals.  Every
 block's bytes and status are compared with the oracle, and each batch is
 decoded through every route: the sidecar segments, the sidecar-less serial
 decoder, and the serial decoder that rebuilds the sidecar."""
+import os
+
 import numpy as np
 import pytest
 
@@ -41,18 +43,19 @@ def _block(rng, n):
     return rng.integers(0, 256, n).astype(np.uint8)  # near-uniform full alphabet
 
 
-@pytest.mark.parametrize("case", range(48))
+# FSEHIP_FUZZ_CASES / FSEHIP_FUZZ_SEED widen the sweep for a one-off run (default: 48 cases)
+@pytest.mark.parametrize("case", range(int(os.environ.get("FSEHIP_FUZZ_CASES", 48))))
 def test_random_batches(torch_cuda, case):
     torch = torch_cuda
     from entropy_coders_amd import BlockCodec
     from entropy_coders_amd._lib import STATUS
 
-    rng = np.random.default_rng(0xF0220 + case)
+    rng = np.random.default_rng(int(os.environ.get("FSEHIP_FUZZ_SEED", 0xF0220)) + case)
     nstates = int(rng.choice([1, 2]))
     block = int(rng.choice([512, 1040, 4096, 20000, 65536]))
     nblocks = int(rng.integers(1, 9))
     last = int(rng.integers(2, block + 1))
-    table_log = 0 if nstates == 1 else int(rng.choice([0, 0, 5, 7, 9, 11, 12, 13, 15]))
+    table_log = 0 if nstates == 1 else int(rng.choice([0, 0, 5, 7, 9, 11, 12, 13, 14, 15]))
     ckpt = int(rng.choice([0, 64, 128, 256]))
     sizes = [block] * (nblocks - 1) + [last]
     blocks = [_block(rng, s) for s in sizes]
@@ -85,10 +88,17 @@ def test_random_batches(torch_cuda, case):
         assert est[b] == 0, (what, STATUS.get(int(est[b])))
         assert codec.block_bytes(cb, b) == want, what
         assert int(cb["payload_bits"][b]) == wbits, what
+        # the reference's own decode of its bytes: the source, except at L = 15
+        # when new_first_symbol's wrapped index lands on another symbol's state
+        # (fse.rs:210-218): then the crate's round trip changes the last symbols,
+        # and the GPU must decode as the crate does
+        ref = s
+        if nstates == 2 and table_log == 15:
+            ref = np.frombuffer(O.decompress2(want, raw_len=len(s)), np.uint8)
         lo = b * block
         for name, (out, st) in routes:
             assert int(st[b]) == 0, (name, what, STATUS.get(int(st[b])))
-            assert np.array_equal(out[lo: lo + len(s)].cpu().numpy(), s), (name, what)
+            assert np.array_equal(out[lo: lo + len(s)].cpu().numpy(), ref), (name, what)
         if ckpt:
             side = rebuilt[1]
             assert torch.equal(side[b * spb: (b + 1) * spb], cb["sidecar"][b * spb: (b + 1) * spb]), what
