@@ -202,18 +202,23 @@ __device__ __forceinline__ int32_t decode_segment1(WindowReader& br, uint32_t& s
 }
 
 // ------------------------------------------------------------------------
-// Segment decode of a block staged in LDS (L <= 12, SH = 18).  One LdsChain
+// Segment decode of a block staged in LDS (L <= 14, SH = 18).  One LdsChain
 // is one segment's decoder pair: two tANS states as LDS byte offsets
 // a0/a1 (4 * state) and the shared bit position.  Per pair the lane reads
 // both table entries and ONE payload dword, all three issued together:
-// a pair consumes <= 24 < 32 bits, so the window base lo = (pos - 24) & ~31
-// moves down by at most one word per pair and the window's upper word is
-// one of the previous pair's two words.  Then pos -= nb0 + nb1 (byte sum of
+// a pair consumes <= 2L <= 28 < 32 bits, so the window base
+// lo = (pos - 28) & ~31 (pos - lo in [28, 59]: the pair's bits and the
+// 64-bit window both fit) moves down by at most one word per pair and the
+// window's upper word is one of the previous pair's two words.  (It was
+// pos - 24 while only L <= 12 ran here: at L = 13 and 14 a pair of rare
+// symbols takes 26 or 28 bits and then read below the window; the wide
+// randomized sweep found one.)  Then pos -= nb0 + nb1 (byte sum of
 // the entries), v1 = the low nb1 bits at pos, v0 = the nb0 bits above
 // (stack order: decoder 0 pops first), and the next offsets.  ~13 VALU and
 // 3 LDS reads per pair, no branch.  The image has a 16-byte pad below it,
 // so the window may start at word -1.
 // ------------------------------------------------------------------------
+constexpr int32_t PAIR_MAX_BITS = 28;  // 2 x 14: the largest pair at the LDS-staged table logs
 struct LdsChain {
     int32_t pos, B;
     uint32_t whi, wlo, a0, a1;
@@ -222,12 +227,12 @@ struct LdsChain {
         a0 = s0 << 2;
         a1 = s1 << 2;
         // the first pair reads word lo/32 and takes word lo/32 + 1 from here
-        B = (p - 24) & ~31;
+        B = (p - PAIR_MAX_BITS) & ~31;
         wlo = 0;
         whi = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(pay) + (B >> 3) + 4);
     }
     __device__ __forceinline__ uint32_t pair(const uint32_t* pay, const uint8_t* dtb) {
-        const int32_t lo = (pos - 24) & ~31;
+        const int32_t lo = (pos - PAIR_MAX_BITS) & ~31;
 #if FSEHIP_ABL & 1  // ablation (timing only, wrong output): conflict-free payload reads
         const int32_t wabl = max(((lo >> 5) & ~31) + (int32_t)(__builtin_amdgcn_workitem_id_x() & 31u), 0);
         const uint32_t w0 = pay[wabl];

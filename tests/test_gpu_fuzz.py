@@ -46,11 +46,27 @@ def _block(rng, n):
 # FSEHIP_FUZZ_CASES / FSEHIP_FUZZ_SEED widen the sweep for a one-off run (default: 48 cases)
 @pytest.mark.parametrize("case", range(int(os.environ.get("FSEHIP_FUZZ_CASES", 48))))
 def test_random_batches(torch_cuda, case):
+    _random_batch(torch_cuda, int(os.environ.get("FSEHIP_FUZZ_SEED", 0xF0220)), case)
+
+
+# cases the wide sweeps found: (seed, case) -> what they caught
+REGRESSIONS = [
+    (77000, 3),  # L = 15: the crate's own decode changes the last symbols (new_first_symbol)
+    (910000, 107),  # L = 13, LDS-staged segments: a 26-bit pair below the old 24-bit window
+]
+
+
+@pytest.mark.parametrize("seed,case", REGRESSIONS)
+def test_random_batch_regressions(torch_cuda, seed, case):
+    _random_batch(torch_cuda, seed, case)
+
+
+def _random_batch(torch_cuda, seed, case):
     torch = torch_cuda
     from entropy_coders_amd import BlockCodec
     from entropy_coders_amd._lib import STATUS
 
-    rng = np.random.default_rng(int(os.environ.get("FSEHIP_FUZZ_SEED", 0xF0220)) + case)
+    rng = np.random.default_rng(seed + case)
     nstates = int(rng.choice([1, 2]))
     block = int(rng.choice([512, 1040, 4096, 20000, 65536]))
     nblocks = int(rng.integers(1, 9))
