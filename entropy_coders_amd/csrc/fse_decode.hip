@@ -928,8 +928,9 @@ __global__ __launch_bounds__(64) void decode1_serial_kernel(DecParams P) {
             const uint32_t e = dt[s];
             const uint32_t nb = dte_nb(e);
             if (br.pos - (int32_t)nb < hdr_bits) break;  // decode_symbol -> None
-            if (o >= cap) {  // nb == 0 forever: a probability-1 symbol never ends in the reference
-                err = nb == 0 ? FSE_ERR_SINGLE_SYMBOL : FSE_ERR_DST_TOO_SMALL;
+            if (o >= cap) {  // a single-symbol table never ends in the reference (the oracle refuses
+                             // it up front); any other stream simply needs more room
+                err = single ? FSE_ERR_SINGLE_SYMBOL : FSE_ERR_DST_TOO_SMALL;
                 break;
             }
             s = Dte<LMAX>::ns(e) + br.pop(nb);
@@ -1527,8 +1528,9 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
                 record_at(pos, s0, 0u);
                 const uint32_t nb = T.nb(s0);
                 if (pos - (int32_t)nb < hdr_bits) break;  // decode_symbol -> None
-                if (o >= lim) {  // nb == 0 forever: a probability-1 symbol never ends in the reference
-                    err = nb == 0 ? FSE_ERR_SINGLE_SYMBOL : FSE_ERR_DST_TOO_SMALL;
+                if (o >= lim) {  // a single-symbol table never ends in the reference (the oracle
+                                 // refuses it up front); any other stream simply needs more room
+                    err = single ? FSE_ERR_SINGLE_SYMBOL : FSE_ERR_DST_TOO_SMALL;
                     break;
                 }
                 const uint32_t y = T.symbol(s0);

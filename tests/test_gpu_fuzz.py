@@ -121,14 +121,14 @@ def _random_batch(torch_cuda, seed, case):
     assert n == sum(sizes)
 
 
-@pytest.mark.parametrize("case", range(16))
+@pytest.mark.parametrize("case", range(int(os.environ.get("FSEHIP_FUZZ_HOST_CASES", 16))))
 def test_random_host_calls(torch_cuda, case):
     """The reference-shaped host entry points on random blocks: fse_compress2
     (and with an explicit table log, clamped as Histogram::normalize does),
     fse_decompress2, fse_compress, fse_decompress, against the oracle."""
     from entropy_coders_amd import FseError, compress, compress2, compress2_log, decompress, decompress2
 
-    rng = np.random.default_rng(0xA110 + case)
+    rng = np.random.default_rng(int(os.environ.get("FSEHIP_FUZZ_SEED", 0xA110)) + case)
     s = _block(rng, int(rng.integers(2, 65537)))
     L = int(rng.integers(0, 21))
     for enc, ref, dec, rdec in ((compress2, O.compress2, decompress2, O.decompress2),
@@ -150,15 +150,27 @@ def test_random_host_calls(torch_cuda, case):
             assert dec(got) == rdec(want), (case, L)
 
 
+@pytest.mark.parametrize("rep", range(int(os.environ.get("FSEHIP_FUZZ_STREAM_REPS", 1))))
 @pytest.mark.parametrize("nstates", [2, 1])
-def test_decompress_streams(torch_cuda, nstates):
+def test_decompress_streams(torch_cuda, nstates, rep):
     """fsehip_decompress_streams: a batch of crate streams of random sizes (no
     sidecar, no raw length), some damaged, some single-symbol, some above
     the table-log limit, each decoded as the crate's fse_decompress2 /
     fse_decompress (reference mode, the oracle) would within the stride."""
+    _streams_case(nstates, 0x57AE + nstates + 2 * rep + int(os.environ.get("FSEHIP_FUZZ_SEED", 0)))
+
+
+# a wide sweep's finding: a 1-state stream longer than the stride whose state
+# at the cut has nb = 0 was reported SINGLE_SYMBOL instead of DST_TOO_SMALL
+@pytest.mark.parametrize("seed", [0x57AE + 1 + 2 * 13 + 123000, 0x57AE + 1 + 2 * 23 + 123000])
+def test_decompress_streams_regressions(torch_cuda, seed):
+    _streams_case(1, seed)
+
+
+def _streams_case(nstates, seed):
     from entropy_coders_amd import decompress_streams
 
-    rng = np.random.default_rng(0x57AE + nstates)
+    rng = np.random.default_rng(seed)
     streams, logs = [], []
     for i in range(60):
         s = _block(rng, int(rng.integers(2, 20000)))
