@@ -265,7 +265,7 @@ typedef struct {
     uint32_t ckpt_interval; /* steps between decode checkpoints (power of two; >= 8 for 2-state
                                pairs, >= 16 for 1-state symbols), 0 = none */
     uint32_t max_table_log; /* upper bound on L used by the blocks (5..15; kernels exist for <= 11,
-                               12 and <= 15); 0 = derive (encode) / 12 (decode) */
+                               12, 13, 14 and 15); 0 = derive (encode) / 12 (decode) */
     uint32_t nstates;       /* block format: 2 (or 0) = fse_compress2 (lib.rs:146), 1 = fse_compress (lib.rs:112) */
 } fsehip_params;
 

@@ -50,6 +50,7 @@ def test_random_batches(torch_cuda, case):
 
 
 # cases the wide sweeps found: (seed, case) -> what they caught
+# (draw version 1: the block-size and checkpoint lists those sweeps used)
 REGRESSIONS = [
     (77000, 3),  # L = 15: the crate's own decode changes the last symbols (new_first_symbol)
     (910000, 107),  # L = 13, LDS-staged segments: a 26-bit pair below the old 24-bit window
@@ -58,23 +59,35 @@ REGRESSIONS = [
 
 @pytest.mark.parametrize("seed,case", REGRESSIONS)
 def test_random_batch_regressions(torch_cuda, seed, case):
-    _random_batch(torch_cuda, seed, case)
+    _random_batch(torch_cuda, seed, case, draw=1)
 
 
-def _random_batch(torch_cuda, seed, case):
+def draw_case(seed, case, draw=2):
+    """The batch of (seed, case): (nstates, block, table_log, ckpt, sizes,
+    blocks).  draw 1: the lists of the sweeps that found REGRESSIONS; draw 2
+    adds 128 KiB blocks (the windowed reader above the 66 KiB stage) and 8..32
+    checkpoints (several segment rounds per workgroup)."""
+    rng = np.random.default_rng(seed + case)
+    nstates = int(rng.choice([1, 2]))
+    block = int(rng.choice([512, 1040, 4096, 20000, 65536] if draw == 1 else [512, 1040, 4096, 20000, 65536, 65536, 131072]))
+    nblocks = int(rng.integers(1, 9))
+    last = int(rng.integers(2, block + 1))
+    table_log = 0 if nstates == 1 else int(rng.choice([0, 0, 5, 7, 9, 11, 12, 13, 14, 15]))
+    if draw == 1:
+        ckpt = int(rng.choice([0, 64, 128, 256]))
+    else:
+        ckpt = int(rng.choice([0, 16, 32, 64, 64, 128, 256] if nstates == 1 else [0, 8, 16, 32, 64, 64, 128, 256]))
+    sizes = [block] * (nblocks - 1) + [last]
+    blocks = [_block(rng, s) for s in sizes]
+    return nstates, block, table_log, ckpt, sizes, blocks
+
+
+def _random_batch(torch_cuda, seed, case, draw=2):
     torch = torch_cuda
     from entropy_coders_amd import BlockCodec
     from entropy_coders_amd._lib import STATUS
 
-    rng = np.random.default_rng(seed + case)
-    nstates = int(rng.choice([1, 2]))
-    block = int(rng.choice([512, 1040, 4096, 20000, 65536]))
-    nblocks = int(rng.integers(1, 9))
-    last = int(rng.integers(2, block + 1))
-    table_log = 0 if nstates == 1 else int(rng.choice([0, 0, 5, 7, 9, 11, 12, 13, 14, 15]))
-    ckpt = int(rng.choice([0, 64, 128, 256]))
-    sizes = [block] * (nblocks - 1) + [last]
-    blocks = [_block(rng, s) for s in sizes]
+    nstates, block, table_log, ckpt, sizes, blocks = draw_case(seed, case, draw)
     host = np.concatenate(blocks)
     n = len(host)
 

@@ -9,20 +9,13 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from entropy_coders_amd import BlockCodec  # noqa: E402
-from tests.test_gpu_fuzz import _block  # noqa: E402
+from tests.test_gpu_fuzz import draw_case  # noqa: E402
 
 seed, case = int(sys.argv[1]), int(sys.argv[2])
-rng = np.random.default_rng(seed + case)
-nstates = int(rng.choice([1, 2]))
-block = int(rng.choice([512, 1040, 4096, 20000, 65536]))
-nblocks = int(rng.integers(1, 9))
-last = int(rng.integers(2, block + 1))
-table_log = 0 if nstates == 1 else int(rng.choice([0, 0, 5, 7, 9, 11, 12, 13, 14, 15]))
-ckpt = int(rng.choice([0, 64, 128, 256]))
-sizes = [block] * (nblocks - 1) + [last]
-blocks = [_block(rng, s) for s in sizes]
+draw = int(sys.argv[3]) if len(sys.argv) > 3 else 2
+nstates, block, table_log, ckpt, sizes, blocks = draw_case(seed, case, draw)
 host = np.concatenate(blocks)
-print("case", nstates, block, nblocks, last, table_log, ckpt, flush=True)
+print("case", nstates, block, len(sizes), sizes[-1], table_log, ckpt, flush=True)
 codec = BlockCodec(block_size=block, table_log=table_log, ckpt_interval=ckpt, nstates=nstates)
 src = torch.from_numpy(host).cuda()
 cb = codec.compress(src)
