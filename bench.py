@@ -448,13 +448,20 @@ def main():
     if world > 1 and not args.no_gather:
         try:
             gather_info = c4_exchange(args, codec, cb, src, world, rank, dev, cdev, backend, barrier)
-            ok = ok and gather_info["verified"]
         except Exception as e:  # reported in the line; the timed step above stands on its own checks
             gather_info = {"error": f"{type(e).__name__}: {e}"[:400], "verified": False}
             print(f"rank {rank}: C4 exchange failed: {gather_info['error']}", file=sys.stderr, flush=True)
-        flag = torch.tensor([1 if ok else 0], device=cdev)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        ok = bool(flag.item())
+        # the exchange is outside the timed step: its check (all ranks) is
+        # c4_exchange.verified; verified_roundtrip stays the step's own
+        try:
+            flag = torch.tensor([1 if gather_info["verified"] else 0], device=cdev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            gather_info["verified"] = bool(flag.item())
+        except Exception as e:
+            gather_info["verified"] = False
+            gather_info.setdefault("error", f"{type(e).__name__}: {e}"[:400])
+        if not gather_info["verified"]:
+            print(f"rank {rank}: C4 exchange not verified", file=sys.stderr, flush=True)
 
     # the same blocks decoded without their sidecar (the format the
     # CPU crate writes): serial per block, several blocks per workgroup
