@@ -170,24 +170,33 @@ def test_decompress_streams(torch_cuda, nstates, rep):
     sidecar, no raw length), some damaged, some single-symbol, some above
     the table-log limit, each decoded as the crate's fse_decompress2 /
     fse_decompress (reference mode, the oracle) would within the stride."""
-    _streams_case(nstates, 0x57AE + nstates + 2 * rep + int(os.environ.get("FSEHIP_FUZZ_SEED", 0)))
+    _streams_case(nstates, 0x57AE + nstates + 2 * rep + int(os.environ.get("FSEHIP_FUZZ_SEED", 0)), draw=2)
 
 
 # a wide sweep's finding: a 1-state stream longer than the stride whose state
 # at the cut has nb = 0 was reported SINGLE_SYMBOL instead of DST_TOO_SMALL
 @pytest.mark.parametrize("seed", [0x57AE + 1 + 2 * 13 + 123000, 0x57AE + 1 + 2 * 23 + 123000])
 def test_decompress_streams_regressions(torch_cuda, seed):
-    _streams_case(1, seed)
+    _streams_case(1, seed, draw=1)
 
 
-def _streams_case(nstates, seed):
+def _streams_case(nstates, seed, draw):
+    """60 crate streams of one seed.  draw 1: the lists of the sweep that found
+    the regressions above; draw 2 adds table logs 5..8, 14, 15, longer streams
+    and other strides."""
     from entropy_coders_amd import decompress_streams
 
     rng = np.random.default_rng(seed)
+    stride = 24000 if draw == 1 else int(rng.choice([24000, 40016, 65536]))
     streams, logs = [], []
     for i in range(60):
-        s = _block(rng, int(rng.integers(2, 20000)))
-        L = int(rng.choice([0, 0, 0, 9, 12, 13])) if nstates == 2 else 0
+        s = _block(rng, int(rng.integers(2, 20000 if draw == 1 else 48000)))
+        if nstates == 1:
+            L = 0
+        elif draw == 1:
+            L = int(rng.choice([0, 0, 0, 9, 12, 13]))
+        else:
+            L = int(rng.choice([0, 0, 0, 5, 8, 9, 11, 12, 13, 14, 15]))
         try:
             comp = O.compress2(s, L or None)[0] if nstates == 2 else O.compress(s)[0]
         except O.OracleError:
@@ -197,7 +206,6 @@ def _streams_case(nstates, seed):
             comp[int(rng.integers(0, len(comp)))] ^= 0x5A
         streams.append(bytes(comp))
         logs.append((comp[0] & 15) + 5)
-    stride = 24000
     ref_dec = O.decompress2 if nstates == 2 else O.decompress
     for mtl in (11, 15):
         got = decompress_streams(streams, stride, nstates=nstates, max_table_log=mtl)
