@@ -258,3 +258,65 @@ def test_random_corruption_never_hangs(torch_cuda, seed, nstates):
     out, side2, st2 = codec.build_sidecar(cb)
     torch.cuda.synchronize()
     assert int(st2.max()) <= 0
+
+
+def test_large_single_blocks(torch_cuda):
+    """Blocks of megabytes (the reference compresses a whole buffer as one
+    block, lib.rs:146-183): the host entry points on a 3 MiB + 17 and a 16 MiB
+    buffer, and a batch of 8 MiB blocks (ragged last) through every decode
+    route: sidecar segments (many rounds per workgroup, payload through the
+    global window), sidecar-less serial, and the rebuilt sidecar."""
+    torch = torch_cuda
+    from entropy_coders_amd import BlockCodec, compress2, decompress2
+
+    for n, p, seed in ((3 * 2**20 + 17, 0.155, 0x1A96E01), (16 * 2**20, 0.5, 0x1A96E02)):
+        s = O.generate(0, p, seed, 0, n)
+        want, wbits = O.compress2(s)
+        got, bits = compress2(s)
+        assert got == want and bits == wbits, n
+        assert decompress2(got) == s.tobytes(), n
+    B = 8 * 2**20
+    blocks = [O.generate(0, 0.155, 0x1A96E03, 0, B), O.generate(2, 0.0, 0x1A96E04, 0, B),
+              O.generate(0, 0.77, 0x1A96E05, 0, 3 * 2**20 + 5)]
+    host = np.concatenate(blocks)
+    for ckpt in (64, 256):
+        codec = BlockCodec(block_size=B, ckpt_interval=ckpt)
+        cb = codec.compress(torch.from_numpy(host).cuda())
+        routes = [codec.decompress(cb), codec.decompress(cb, use_sidecar=False)]
+        rebuilt = codec.build_sidecar(cb)
+        routes.append(rebuilt[::2])
+        torch.cuda.synchronize()
+        spb = codec.side_per_block
+        for b, s in enumerate(blocks):
+            want, wbits = O.compress2(s)
+            assert int(cb["status"][b]) == 0, (ckpt, b)
+            assert codec.block_bytes(cb, b) == want, (ckpt, b)
+            assert int(cb["payload_bits"][b]) == wbits, (ckpt, b)
+            assert torch.equal(rebuilt[1][b * spb: (b + 1) * spb], cb["sidecar"][b * spb: (b + 1) * spb]), (ckpt, b)
+            for r, (out, st) in enumerate(routes):
+                assert int(st[b]) == 0, (ckpt, b, r)
+                assert torch.equal(out[b * B: b * B + len(s)].cpu(), torch.from_numpy(s)), (ckpt, b, r)
+
+
+def test_max_block_size(torch_cuda):
+    """The largest block the batched path takes (2^28 bytes: bit positions are
+    32-bit, fsehip.h), exact against the oracle and decoded through its
+    sidecar; one byte-group more is UNSUPPORTED, not a wrong result."""
+    torch = torch_cuda
+    from entropy_coders_amd import BlockCodec, FseError
+
+    B = 1 << 28
+    s = O.generate(0, 0.155, 0x1A96E06, 0, B)
+    want, wbits = O.compress2(s)
+    codec = BlockCodec(block_size=B, ckpt_interval=256)
+    src = torch.from_numpy(s).cuda()
+    cb = codec.compress(src)
+    out, st = codec.decompress(cb)
+    torch.cuda.synchronize()
+    assert int(cb["status"][0]) == 0 and int(st[0]) == 0
+    assert int(cb["payload_bits"][0]) == wbits
+    assert codec.block_bytes(cb, 0) == want
+    assert torch.equal(out, src)
+    with pytest.raises(FseError) as g:
+        BlockCodec(block_size=B + 16, ckpt_interval=256).compress(src[:4096])
+    assert g.value.code == "UNSUPPORTED"
