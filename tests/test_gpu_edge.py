@@ -320,3 +320,35 @@ def test_max_block_size(torch_cuda):
     with pytest.raises(FseError) as g:
         BlockCodec(block_size=B + 16, ckpt_interval=256).compress(src[:4096])
     assert g.value.code == "UNSUPPORTED"
+
+
+def test_large_blocks_one_state(torch_cuda):
+    """The 1-state format (fse_compress, lib.rs:112-143) on megabyte blocks:
+    the host calls on 5 MiB, and 8 MiB batch blocks through every route."""
+    torch = torch_cuda
+    from entropy_coders_amd import BlockCodec, compress, decompress
+
+    s = O.generate(0, 0.3, 0x1A96E07, 0, 5 * 2**20 + 3)
+    want, wbits = O.compress(s)
+    got, bits = compress(s)
+    assert got == want and bits == wbits
+    assert decompress(got) == s.tobytes()
+    B = 8 * 2**20
+    blocks = [O.generate(0, 0.155, 0x1A96E08, 0, B), O.generate(0, 0.6, 0x1A96E09, 0, 2**20 + 9)]
+    host = np.concatenate(blocks)
+    codec = BlockCodec(block_size=B, ckpt_interval=128, nstates=1)
+    cb = codec.compress(torch.from_numpy(host).cuda())
+    routes = [codec.decompress(cb), codec.decompress(cb, use_sidecar=False)]
+    rebuilt = codec.build_sidecar(cb)
+    routes.append(rebuilt[::2])
+    torch.cuda.synchronize()
+    spb = codec.side_per_block
+    for b, s in enumerate(blocks):
+        want, wbits = O.compress(s)
+        assert int(cb["status"][b]) == 0, b
+        assert codec.block_bytes(cb, b) == want, b
+        assert int(cb["payload_bits"][b]) == wbits, b
+        assert torch.equal(rebuilt[1][b * spb: (b + 1) * spb], cb["sidecar"][b * spb: (b + 1) * spb]), b
+        for r, (out, st) in enumerate(routes):
+            assert int(st[b]) == 0, (b, r)
+            assert torch.equal(out[b * B: b * B + len(s)].cpu(), torch.from_numpy(s)), (b, r)
