@@ -237,7 +237,9 @@ int bitstack_writer_write_bits_raw(fse_bitstack_writer* w, uint32_t val, uint32_
         const int rc = bitstack_writer_flush(w);
         if (rc) return rc;
     }
-    w->storage |= (uint64_t)val << w->bits;
+    // a 0-bit write after 64 pending bits (possible without a flush) would
+    // shift by 64
+    if (nbits) w->storage |= (uint64_t)val << w->bits;
     w->bits += nbits;
     return FSE_OK;
 }
