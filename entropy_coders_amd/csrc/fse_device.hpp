@@ -655,15 +655,26 @@ __device__ inline int header_read_lane(const uint32_t* src, uint32_t n, uint32_t
 // NormHistogram::read (histogram.rs:436-505) as wave-uniform code: every lane
 // of the calling wave holds the same values, so the serial parse runs on the
 // scalar unit (s_lshr_b64 window, s_flbit for the threshold) instead of one
-// VALU lane.  Words come from LDS through readfirstlane.  norm[] must be
-// zeroed by the caller; lane 0 stores the parsed entries.  Same results and
-// statuses as header_read_lane.
+// VALU lane.  norm[] must be zeroed by the caller.  Same results and statuses
+// as header_read_lane.
+//
+// The scalar unit is shared by the CU's waves, and the decode-table kernel is
+// bound by its issue rate (the parse is ~90% of that kernel's scalar
+// instructions), so the common field is a straight run of scalar code: every
+// error here is BAD_HEADER, so the end-of-data check is deferred (left only
+// falls; reads past the data see zeros and the loop still ends within 256
+// symbols), the threshold is recomputed unconditionally (thr = 2^ilog2(rem)
+// holds throughout, the closed form of 492-495), every lane stores the same
+// norm value (no exec-mask change), and the zero-run marks (456-464) and the
+// loop's end conditions leave the common path through one branch.
 // ---------------------------------------------------------------------------
 __device__ inline int header_read_wave(uint32_t r0, uint32_t r1, uint32_t n, uint32_t lmax, int32_t* norm,
                                        uint32_t* L_out, uint32_t* tl_out) {
     if (n == 0) return FSE_ERR_EMPTY;
-    const uint32_t lane = lane_id();
-    const int32_t total = (int32_t)(n * 8u);
+    // a header is at most ~420 bytes: bounding the bit count keeps it in
+    // int32 for any block (n*8 overflows above 2^28 bytes) without changing
+    // where the header can run out
+    const int32_t total = (int32_t)(min(n, 1u << 20) * 8u);
     // r0 / r1 hold header words lane / 64 + lane (zero past the block): a
     // word is one v_readlane.  Headers of L <= 12 fit in 417 bytes, so the
     // 512 bytes held always cover them (L > lmax returns before reading on).
@@ -690,58 +701,55 @@ __device__ inline int header_read_wave(uint32_t r0, uint32_t r1, uint32_t n, uin
     if (L > LOG_MAX_REF) return FSE_ERR_BAD_HEADER;  // TableLogTooLarge
     if (L > lmax) return FSE_ERR_UNSUPPORTED;          // valid for the crate, beyond this build's tables
     uint32_t sym = 0, rem = (1u << L) + 1u, lg = L, thr = 1u << L;  // read width = lg + 1
-    bool prev0 = false;
-    while (rem > 1u && sym < 256u) {
-        if (prev0) {  // zero-run marks (456-464): peek(..).unwrap_or(0)
-            for (;;) {
-                refill();
-                if (left < 16 || ((uint32_t)(buf >> off) & 0xFFFFu) != 0xFFFFu) break;
-                off += 16u;
-                left -= 16;
-                sym += 24u;
-            }
-            for (;;) {
-                refill();
-                if (left < 2 || ((uint32_t)(buf >> off) & 3u) != 3u) break;
-                off += 2u;
-                left -= 2;
-                sym += 3u;
-            }
-            if (left < 2) return FSE_ERR_BAD_HEADER;
-            sym += (uint32_t)(buf >> off) & 3u;
-            off += 2u;
-            left -= 2;
-            if (sym >= 256u) break;
-        }
+    for (;;) {  // entered with rem > 1 and sym < 256
         refill();
         // peek(nb) falling back to peek(nb-1) (471-473): the short path only
-        // uses the low nb-1 bits, and the long path needs all nb, so one
-        // bound check on the advance covers both
+        // uses the low nb-1 bits and the long path needs all nb, so "left <
+        // the advance" is the reference's error for both
         const uint32_t raw = (uint32_t)(buf >> off);
-        const uint32_t mx = (2u * thr - 1u) - rem;
+        const uint32_t t2 = 2u * thr - 1u;
+        const uint32_t mx = t2 - rem;
         const uint32_t low = raw & (thr - 1u);
-        uint32_t val, adv;
-        if (low < mx) {
-            adv = lg;
-            val = low;
-        } else {
-            adv = lg + 1u;
-            val = raw & (2u * thr - 1u);
-            if (val >= thr) val -= mx;
-        }
-        if (left < (int32_t)adv) return FSE_ERR_BAD_HEADER;
+        uint32_t vlong = raw & t2;
+        vlong = vlong >= thr ? vlong - mx : vlong;
+        const bool lng = low >= mx;
+        const uint32_t val = lng ? vlong : low;
+        const uint32_t adv = lg + (lng ? 1u : 0u);
         off += adv;
         left -= (int32_t)adv;
         const int32_t sv = (int32_t)val - 1;
-        rem -= (uint32_t)(sv < 0 ? -sv : sv);
-        if (lane == 0) norm[sym] = sv;
+        rem -= (uint32_t)__builtin_abs(sv);  // stays >= 1 (val <= rem)
+        norm[sym] = sv;
         sym += 1u;
-        prev0 = sv == 0;
-        if (rem < thr) {  // the halving loop of 492-495 in closed form
-            lg = ilog2u(rem);
-            thr = 1u << lg;
+        lg = 31u - (uint32_t)__builtin_clz(rem);
+        thr = 1u << lg;
+        // leave the common path after a 0 (val == 1), at rem == 1 or at
+        // symbol 256, as one test: rem <= 2^15 + 1 and val <= 2^16, so bit 31
+        // of rem - 2 and of (val ^ 1) - 1 is set exactly when rem < 2, val == 1
+        if ((((rem - 2u) | ((val ^ 1u) - 1u)) >> 31 | (sym >> 8)) == 0u) continue;
+        if (rem <= 1u || sym >= 256u) break;
+        // zero-run marks after a 0 (456-464): peek(..).unwrap_or(0)
+        for (;;) {
+            refill();
+            if (left < 16 || ((uint32_t)(buf >> off) & 0xFFFFu) != 0xFFFFu) break;
+            off += 16u;
+            left -= 16;
+            sym += 24u;
         }
+        for (;;) {
+            refill();
+            if (left < 2 || ((uint32_t)(buf >> off) & 3u) != 3u) break;
+            off += 2u;
+            left -= 2;
+            sym += 3u;
+        }
+        if (left < 2) return FSE_ERR_BAD_HEADER;
+        sym += (uint32_t)(buf >> off) & 3u;
+        off += 2u;
+        left -= 2;
+        if (sym >= 256u) break;
     }
+    if (left < 0) return FSE_ERR_BAD_HEADER;   // a field ran past the data (UnexpectedEof)
     if (rem != 1u) return FSE_ERR_BAD_HEADER;  // TooManySymbols
     *L_out = L;
     *tl_out = sym;
