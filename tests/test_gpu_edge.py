@@ -304,6 +304,7 @@ def test_max_block_size(torch_cuda):
     sidecar; one byte-group more is UNSUPPORTED, not a wrong result."""
     torch = torch_cuda
     from entropy_coders_amd import BlockCodec, FseError
+    from entropy_coders_amd._lib import STATUS
 
     B = 1 << 28
     s = O.generate(0, 0.155, 0x1A96E06, 0, B)
@@ -320,6 +321,18 @@ def test_max_block_size(torch_cuda):
     with pytest.raises(FseError) as g:
         BlockCodec(block_size=B + 16, ckpt_interval=256).compress(src[:4096])
     assert g.value.code == "UNSUPPORTED"
+    # an incompressible 2^28-byte block encodes exactly, but its compressed
+    # stream (> 2^28 bytes) is beyond the decoders' 32-bit bit positions:
+    # UNSUPPORTED, on every route, never wrong bytes
+    del out, src, cb
+    s = np.random.default_rng(7).integers(0, 256, B, dtype=np.uint8)
+    want, wbits = O.compress2(s)
+    assert len(want) > B
+    cb = codec.compress(torch.from_numpy(s).cuda())
+    assert int(cb["status"][0]) == 0 and codec.block_bytes(cb, 0) == want
+    for use_sidecar in (True, False):
+        _, st = codec.decompress(cb, use_sidecar=use_sidecar)
+        assert STATUS.get(int(st[0])) == "UNSUPPORTED", use_sidecar
 
 
 def test_large_blocks_one_state(torch_cuda):
