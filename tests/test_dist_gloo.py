@@ -1,4 +1,4 @@
-"""world_size-2 (and 3) gloo tests of the multi-GPU exchange on CPU: block
+"""world_size 2, 3, 4 and 8 gloo tests of the multi-GPU exchange on CPU: block
 sharding, the compressed-output gatherv and the scatter for distributed
 decode, with blocks produced by the CPU oracle (test checker) standing in for
 each rank's GPU output.  The same functions run over RCCL on MI355X
@@ -87,7 +87,8 @@ def _worker(rank, world, port, scheme, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("scheme,world", [("contiguous", 2), ("round_robin", 2), ("round_robin", 3)])
+@pytest.mark.parametrize("scheme,world", [("contiguous", 2), ("round_robin", 2), ("round_robin", 3),
+                                          ("contiguous", 4), ("round_robin", 8)])
 def test_gather_scatter(scheme, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
