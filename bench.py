@@ -24,6 +24,7 @@ import os
 import socket
 import subprocess
 import sys
+import threading
 import time
 
 import numpy as np
@@ -69,6 +70,9 @@ def parse():
     ap.add_argument("--no-gather", action="store_true",
                     help="N > 1: skip the gather of the compressed shards to rank 0 and the scatter back "
                          "(reported separately, never in value)")
+    ap.add_argument("--gather-timeout", type=float, default=180.0,
+                    help="N > 1: seconds the exchange may take; past that every rank ends (rank 0 first "
+                         "prints the line, the exchange marked as timed out) instead of hanging in a collective")
     ap.add_argument("--scheme", default="round_robin", choices=("round_robin", "contiguous"),
                     help="block -> rank mapping of the gather/scatter (C4: block b on GPU b mod N)")
     return ap.parse_args()
@@ -444,8 +448,64 @@ def main():
 
     # C4 exchange (N > 1): gatherv of the compressed shards to rank 0, then the
     # scatter back for distributed decode; verified by decoding what came back
+    enc_bytes = n + comp_bytes + side_bytes  # raw read + compressed (+ sidecar) written
+    dec_bytes = comp_bytes + side_bytes + n  # compressed (+ sidecar) read + raw written
+
+    def step_line() -> dict:  # the timed step's part of the line
+        line = {
+            "metric": METRIC,
+            "value": round(job_bytes * args.steps / elapsed / 2**30, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong" if args.strong else "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {
+                "workload": workload_name(args, args.bytes if args.strong else n),
+                "format": "2-state (fse_compress2)" if args.nstates == 2 else "1-state (fse_compress)",
+                "block_size": args.block,
+                "bytes_per_gpu": n,
+                "table_log": args.table_log or "optimal (11)",
+                "ckpt_interval": f"{args.ckpt} {'pairs' if args.nstates == 2 else 'symbols'}",
+                "parallelism": f"dp{world} (blocks sharded per GPU, no collective in the step)",
+            },
+            # dominant kernel of the step: encode (one launch per step)
+            "roofline": roofline("fse_encode_blocks", enc_ms, enc_bytes, "encode launch, HIP events", prof_cfg),
+            "roofline_decode": roofline("fse_decode_blocks", dec_ms, dec_bytes,
+                                        "decode-table + decode launches, HIP events", prof_cfg),
+            "encode_ms": round(enc_ms, 4),
+            "decode_ms": round(dec_ms, 4),
+            "encode_GiB_s": round(n / (enc_ms * 1e-3) / 2**30, 2),
+            "decode_GiB_s": round(n / (dec_ms * 1e-3) / 2**30, 2),
+            "compressed_ratio": round(comp_bytes / n, 5),
+            "verified_roundtrip": ok,
+        }
+        if enc_ms < dec_ms:
+            line["roofline"], line["roofline_decode"] = line["roofline_decode"], line["roofline"]
+        return line
+
     gather_info = None
     if world > 1 and not args.no_gather:
+        # A collective that never completes would hold every rank, and the step's
+        # line with them: past --gather-timeout each rank ends itself (os._exit
+        # from a timer thread; the collectives release the GIL while they wait),
+        # rank 0 after printing the line with the exchange marked timed out.
+        def give_up():
+            if rank == 0:
+                line = step_line()
+                line["c4_exchange"] = {"error": f"no result within {args.gather_timeout:g} s", "verified": False}
+                print(json.dumps(line), flush=True)
+            print(f"rank {rank}: C4 exchange timed out", file=sys.stderr, flush=True)
+            os._exit(0 if ok else 3)
+
+        watchdog = threading.Timer(args.gather_timeout, give_up)
+        watchdog.daemon = True
+        watchdog.start()
         try:
             gather_info = c4_exchange(args, codec, cb, src, world, rank, dev, cdev, backend, barrier)
         except Exception as e:  # reported in the line; the timed step above stands on its own checks
@@ -460,6 +520,7 @@ def main():
         except Exception as e:
             gather_info["verified"] = False
             gather_info.setdefault("error", f"{type(e).__name__}: {e}"[:400])
+        watchdog.cancel()
         if not gather_info["verified"]:
             print(f"rank {rank}: C4 exchange not verified", file=sys.stderr, flush=True)
 
@@ -588,43 +649,7 @@ def main():
         del host_src, hs_stream, h_out, c_out, d_out
 
     if rank == 0:
-        enc_bytes = n + comp_bytes + side_bytes  # raw read + compressed (+ sidecar) written
-        dec_bytes = comp_bytes + side_bytes + n  # compressed (+ sidecar) read + raw written
-        line = {
-            "metric": METRIC,
-            "value": round(job_bytes * args.steps / elapsed / 2**30, 3),
-            "unit": "GiB/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "strong" if args.strong else "weak",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic",
-            "config": {
-                "workload": workload_name(args, args.bytes if args.strong else n),
-                "format": "2-state (fse_compress2)" if args.nstates == 2 else "1-state (fse_compress)",
-                "block_size": args.block,
-                "bytes_per_gpu": n,
-                "table_log": args.table_log or "optimal (11)",
-                "ckpt_interval": f"{args.ckpt} {'pairs' if args.nstates == 2 else 'symbols'}",
-                "parallelism": f"dp{world} (blocks sharded per GPU, no collective in the step)",
-            },
-            # dominant kernel of the step: encode (one launch per step)
-            "roofline": roofline("fse_encode_blocks", enc_ms, enc_bytes, "encode launch, HIP events", prof_cfg),
-            "roofline_decode": roofline("fse_decode_blocks", dec_ms, dec_bytes,
-                                        "decode-table + decode launches, HIP events", prof_cfg),
-            "encode_ms": round(enc_ms, 4),
-            "decode_ms": round(dec_ms, 4),
-            "encode_GiB_s": round(n / (enc_ms * 1e-3) / 2**30, 2),
-            "decode_GiB_s": round(n / (dec_ms * 1e-3) / 2**30, 2),
-            "compressed_ratio": round(comp_bytes / n, 5),
-            "verified_roundtrip": ok,
-        }
-        if enc_ms < dec_ms:
-            line["roofline"], line["roofline_decode"] = line["roofline_decode"], line["roofline"]
+        line = step_line()
         if c3 is not None:
             line["c3_decode_only"] = c3
         if serial is not None:
