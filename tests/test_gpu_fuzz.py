@@ -207,7 +207,7 @@ def _streams_case(nstates, seed, draw):
         streams.append(bytes(comp))
         logs.append((comp[0] & 15) + 5)
     ref_dec = O.decompress2 if nstates == 2 else O.decompress
-    for mtl in (11, 15):
+    for mtl in (11, 12, 13, 14, 15):
         got = decompress_streams(streams, stride, nstates=nstates, max_table_log=mtl)
         for i, (x, g) in enumerate(zip(streams, got)):
             if logs[i] > mtl and logs[i] <= 15:
