@@ -34,7 +34,7 @@ uint64_t round_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 // synchronises the stream (the work of earlier holders has been enqueued on
 // it) before freeing the old one.  Different streams get different
 // workspaces.
-enum { SCRATCH_DT = 0, SCRATCH_DTINFO = 1, SCRATCH_BITS = 2, SCRATCH_KINDS = 3 };
+enum { SCRATCH_DT = 0, SCRATCH_DTINFO = 1, SCRATCH_BITS = 2, SCRATCH_STATES = 3, SCRATCH_BULK = 4, SCRATCH_KINDS = 5 };
 struct Workspace {
     int dev;
     void* stream;
@@ -74,6 +74,7 @@ struct Lease {
             }
             ws->bytes[tag] = 0;
             if (hipMalloc(&ws->ptr[tag], bytes) != hipSuccess) {
+                (void)hipGetLastError();  // an optional buffer's failure must not surface in a later launch check
                 ws->ptr[tag] = nullptr;
                 return nullptr;
             }
@@ -320,13 +321,25 @@ int fsehip_compress_blocks(const fsehip_params* p, const uint8_t* d_src, uint64_
     return e == hipSuccess ? FSE_OK : FSE_ERR_HIP;
 }
 
+// Sidecar-less 2-state decode at L <= 11: the chains defer their symbols to
+// a map kernel when the stream's workspace can hold the state pairs (2 bytes
+// per output byte); without it the single-kernel serial decode runs.
+// FSEHIP_SERIAL_DEFER=0 (diagnostics) always takes the latter.
+static void defer_symbols(Lease& lease, fsehip::DecParams& P, uint32_t lmax) {
+    if (lmax > 11 || P.block_size < 2u || !env_u32("FSEHIP_SERIAL_DEFER", 1)) return;
+    P.states = static_cast<uint32_t*>(lease.get(SCRATCH_STATES, 2ull * P.n_blocks * P.block_size));
+    P.bulk = static_cast<uint32_t*>(lease.get(SCRATCH_BULK, 8ull * P.n_blocks));
+    if (!P.states || !P.bulk) P.states = P.bulk = nullptr;
+}
+
 // Decode on prebuilt tables (dtable_blocks_kernel at stride kern_lmax):
 // segment-parallel with a sidecar, else serial (container mode when n_total
 // is known, the reference's own termination within out_cap otherwise).
 static int decompress_impl(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
                            const uint32_t* d_comp_len, const uint64_t* d_sidecar, uint8_t* d_out, uint64_t n_total,
                            uint64_t* d_sidecar_out, int32_t* d_status, uint32_t* d_out_len, uint32_t out_cap,
-                           fsehip_stream_t stream, const uint32_t* d_dt, const int32_t* d_dtinfo) {
+                           fsehip_stream_t stream, const uint32_t* d_dt, const int32_t* d_dtinfo,
+                           Lease* lease = nullptr) {
     if (!p || !d_in || !d_comp_len || !d_out || !d_status || !d_dt || !d_dtinfo) return FSE_ERR_BAD_ARG;
     const uint32_t bs = p->block_size ? p->block_size : kDefaultBlock;
     if (bs > kMaxBlock) return FSE_ERR_UNSUPPORTED;
@@ -363,6 +376,7 @@ static int decompress_impl(const fsehip_params* p, const uint8_t* d_in, uint64_t
     P.sidecar_out = d_sidecar_out;
     P.dt = d_dt;
     P.dtinfo = d_dtinfo;
+    if (lease && !d_sidecar && !d_sidecar_out && ns == 2) defer_symbols(*lease, P, kern_lmax(p->max_table_log));
     P.stamps = g_stamps_dec.get(n_blocks);
     hipError_t e = fsehip::launch_decode(P, kern_lmax(p->max_table_log), static_cast<hipStream_t>(stream));
     if (P.stamps) g_stamps_dec.report("decode", n_blocks, static_cast<hipStream_t>(stream));
@@ -397,13 +411,17 @@ int fsehip_decompress_blocks_dt(const fsehip_params* p, const uint8_t* d_in, uin
     if (n_total == 0) return FSE_ERR_EMPTY;
     if (!p || !d_dtables || !d_dtinfo) return FSE_ERR_BAD_ARG;
     if (d_sidecar && p->ckpt_interval == 0) return FSE_ERR_BAD_ARG;
-    return decompress_impl(p, d_in, slot_bytes, d_comp_len, d_sidecar, d_out, n_total, nullptr, d_status, nullptr, 0,
-                           stream, d_dtables, d_dtinfo);
+    if (d_sidecar)
+        return decompress_impl(p, d_in, slot_bytes, d_comp_len, d_sidecar, d_out, n_total, nullptr, d_status, nullptr,
+                               0, stream, d_dtables, d_dtinfo);
+    Lease lease(stream);  // the deferred-symbol workspace
+    return decompress_impl(p, d_in, slot_bytes, d_comp_len, nullptr, d_out, n_total, nullptr, d_status, nullptr, 0,
+                           stream, d_dtables, d_dtinfo, &lease);
 }
 
 extern "C++" {
 // Decode tables for all blocks at high occupancy into the stream's
-// workspace, then `run(dt, info)` enqueues the decode on them; both under
+// workspace, then `run(dt, info, lease)` enqueues the decode on them; both under
 // the workspace lock.
 template <class Run>
 static int with_dtables_n(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes, const uint32_t* d_comp_len,
@@ -415,7 +433,7 @@ static int with_dtables_n(const fsehip_params* p, const uint8_t* d_in, uint64_t 
     int32_t* info = static_cast<int32_t*>(lease.get(SCRATCH_DTINFO, 4ull * n_blocks));
     if (!dt || !info) return FSE_ERR_HIP;
     int rc = fsehip_build_dtables(p, d_in, slot_bytes, d_comp_len, (uint32_t)n_blocks, dt, info, stream);
-    return rc != FSE_OK ? rc : run(dt, info);
+    return rc != FSE_OK ? rc : run(dt, info, lease);
 }
 template <class Run>
 static int with_dtables(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes, const uint32_t* d_comp_len,
@@ -432,10 +450,11 @@ int fsehip_decompress_blocks(const fsehip_params* p, const uint8_t* d_in, uint64
     if (n_total == 0) return FSE_ERR_EMPTY;
     if (!p) return FSE_ERR_BAD_ARG;
     if (d_sidecar && p->ckpt_interval == 0) return FSE_ERR_BAD_ARG;
-    return with_dtables(p, d_in, slot_bytes, d_comp_len, n_total, stream, [&](const uint32_t* dt, const int32_t* info) {
-        return fsehip_decompress_blocks_dt(p, d_in, slot_bytes, d_comp_len, d_sidecar, dt, info, d_out, n_total,
-                                           d_status, stream);
-    });
+    return with_dtables(p, d_in, slot_bytes, d_comp_len, n_total, stream,
+                        [&](const uint32_t* dt, const int32_t* info, Lease& lease) {
+                            return decompress_impl(p, d_in, slot_bytes, d_comp_len, d_sidecar, d_out, n_total, nullptr,
+                                                   d_status, nullptr, 0, stream, dt, info, &lease);
+                        });
 }
 
 int fsehip_build_sidecar(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
@@ -447,7 +466,7 @@ int fsehip_build_sidecar(const fsehip_params* p, const uint8_t* d_in, uint64_t s
     // 1-state blocks above L = 12 decode on decode1_serial_kernel, which records nothing
     if (ns == 1 && kern_lmax(p->max_table_log) > 12) return FSE_ERR_UNSUPPORTED;
     if (p->ckpt_interval < (ns == 1 ? 16u : 8u) || (p->ckpt_interval & (p->ckpt_interval - 1))) return FSE_ERR_BAD_ARG;
-    return with_dtables(p, d_in, slot_bytes, d_comp_len, n_total, stream, [&](const uint32_t* dt, const int32_t* info) {
+    return with_dtables(p, d_in, slot_bytes, d_comp_len, n_total, stream, [&](const uint32_t* dt, const int32_t* info, Lease&) {
         return decompress_impl(p, d_in, slot_bytes, d_comp_len, nullptr, d_out, n_total, d_sidecar_out, d_status,
                                nullptr, 0, stream, dt, info);
     });
@@ -464,7 +483,7 @@ int fsehip_decompress_streams(uint32_t nstates, uint32_t max_table_log, const ui
     if (max_table_log > 15) return FSE_ERR_UNSUPPORTED;
     const fsehip_params p{out_stride, 0, 0, max_table_log ? max_table_log : 11u, nstates ? nstates : 2u};
     return with_dtables_n(&p, d_in, in_stride, d_comp_len, n_streams, stream,
-                          [&](const uint32_t* dt, const int32_t* info) {
+                          [&](const uint32_t* dt, const int32_t* info, Lease& lease) {
                               fsehip::DecParams P{};
                               P.nstates = p.nstates;
                               P.in = d_in;
@@ -479,6 +498,7 @@ int fsehip_decompress_streams(uint32_t nstates, uint32_t max_table_log, const ui
                               P.out_len = d_out_len;
                               P.dt = dt;
                               P.dtinfo = info;
+                              if (P.nstates == 2) defer_symbols(lease, P, kern_lmax(p.max_table_log));
                               return fsehip::launch_decode(P, kern_lmax(p.max_table_log),
                                                            static_cast<hipStream_t>(stream)) == hipSuccess
                                          ? (int)FSE_OK

@@ -1261,6 +1261,21 @@ struct RingChain {
         B1 = T.H + T.ns(e1) + v1;
         return y0 | (y1 << 8);
     }
+    // one pair with the symbols deferred: returns the two states (low 16
+    // bits of each halved entry address) for sym_map_kernel
+    __device__ __forceinline__ uint32_t pair_states(const Tab& T) {
+        const uint32_t e0 = T.entry_at(B0), e1 = T.entry_at(B1);
+        const uint32_t v = __builtin_amdgcn_perm(B1, B0, 0x05040100u);
+        const uint32_t x = window();
+        const uint32_t n0 = T.nbf(e0), n1 = T.nbf(e1);
+        const uint32_t o0 = 0u - n0;
+        const uint32_t v0 = __builtin_amdgcn_ubfe(x, o0, n0);
+        const uint32_t v1 = __builtin_amdgcn_ubfe(x, o0 - n1, n1);
+        p32 -= (int32_t)((n0 + n1) & 31u);
+        B0 = T.H + T.ns(e0) + v0;
+        B1 = T.H + T.ns(e1) + v1;
+        return v;
+    }
     // NS = 1: one symbol; returns it
     __device__ __forceinline__ uint32_t step(const Tab& T) {
         const uint32_t e = T.entry_at(B0);
@@ -1273,14 +1288,17 @@ struct RingChain {
     }
 };
 
-template <int LMAX, uint32_t K, int NS>
+template <int LMAX, uint32_t K, int NS, bool DEF = false>
 __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
     static_assert(LMAX <= 12, "entry layout ns << 18: e >> 16 is the next entry's byte offset");
     static_assert(K >= 1 && K <= 64, "one decode lane per block");
+    static_assert(!DEF || (NS == 2 && LMAX <= 11), "deferred symbols: 2-state, L <= 11");
     constexpr uint32_t NBW = LMAX <= 11 ? 5u : 4u;  // nb | newState << NBW fits 16 bits
     constexpr uint32_t TW = 1u << LMAX;
-    // u16 entries of the K blocks, then their u8 symbols
-    __shared__ __attribute__((aligned(16))) uint8_t tab_all[K * 3u * TW];
+    // u16 entries of the K blocks, then their u8 symbols (DEF: entries only;
+    // the symbols are looked up by sym_map_kernel and, for the few end-of-block
+    // steps, in the prebuilt u32 table in HBM)
+    __shared__ __attribute__((aligned(16))) uint8_t tab_all[K * (DEF ? 2u : 3u) * TW];
     __shared__ uint32_t ring_all[K * RING_STRIDE];
     __shared__ int32_t ctl_all[K][2];  // [0] lowest word landed, [1] highest word the decoder may still read; INT32_MIN = stop
     __shared__ uint32_t any_nb[K];
@@ -1312,9 +1330,10 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
             auto c16 = [](uint32_t e) { return (e & 0xFu) | ((e >> (18u - NBW)) & ~((1u << NBW) - 1u)); };
             reinterpret_cast<uint2*>(tb)[i] =
                 make_uint2(c16(q.x) | (c16(q.y) << 16), c16(q.z) | (c16(q.w) << 16));
-            reinterpret_cast<uint32_t*>(sb)[i] =
-                __builtin_amdgcn_perm(__builtin_amdgcn_perm(q.w, q.z, 0x0c0c0501u),
-                                      __builtin_amdgcn_perm(q.y, q.x, 0x0c0c0501u), 0x05040100u);
+            if (!DEF)
+                reinterpret_cast<uint32_t*>(sb)[i] =
+                    __builtin_amdgcn_perm(__builtin_amdgcn_perm(q.w, q.z, 0x0c0c0501u),
+                                          __builtin_amdgcn_perm(q.y, q.x, 0x0c0c0501u), 0x05040100u);
             nbor |= (q.x | q.y | q.z | q.w) & 0xFFu;
         }
         if (nbor) atomicOr(&any_nb[j], 1u);
@@ -1332,10 +1351,17 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
             wj[j] = reinterpret_cast<const uint32_t*>(P.in + (gb0 + j) * P.slot_bytes);
             if (nwj[j] > 0) act |= 1u << j;
         }
+        // one sweep: every ring's chunk loads are issued before the first
+        // ring write waits on them (a sweep that waited ring by ring took
+        // ~K load latencies, near a chunk's decode time at K = 8)
+        constexpr uint32_t NQ = RING_WORDS / RING_CHUNK;
         while (act) {
-            bool moved = false;
+            uint32_t v[K][NQ];
+            int32_t k1s[K];
+            uint32_t mv = 0;
 #pragma unroll
             for (uint32_t j = 0; j < K; ++j) {
+                k1s[j] = k[j];
                 if (!(act & (1u << j))) continue;
                 const int32_t need = lds_load_volatile(&ctl_all[j][1]);
                 if (need == INT32_MIN) {  // the decoder is done (or failed)
@@ -1344,29 +1370,33 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
                 }
                 // chunk c may overwrite the slots of words 64c + RING_WORDS..: dead once above `need`
                 int32_t k1 = k[j];
-                while (k1 >= 0 && k1 > k[j] - (int32_t)(RING_WORDS / RING_CHUNK) &&
-                       k1 * (int32_t)RING_CHUNK + (int32_t)RING_WORDS > need)
+                while (k1 >= 0 && k1 > k[j] - (int32_t)NQ && k1 * (int32_t)RING_CHUNK + (int32_t)RING_WORDS > need)
                     --k1;
                 if (k1 == k[j]) continue;
-                uint32_t v[RING_WORDS / RING_CHUNK];  // all loads in flight before the first LDS write
+                k1s[j] = k1;
 #pragma unroll
-                for (int32_t q = 0; q < (int32_t)(RING_WORDS / RING_CHUNK); ++q) {
+                for (int32_t q = 0; q < (int32_t)NQ; ++q) {
                     const int32_t wi = (k[j] - q) * (int32_t)RING_CHUNK + (int32_t)lane;
-                    v[q] = (k[j] - q > k1 && wi < nwj[j]) ? wj[j][wi] : 0u;
+                    v[j][q] = (k[j] - q > k1 && wi < nwj[j]) ? wj[j][wi] : 0u;
                 }
+                mv |= 1u << j;
+            }
 #pragma unroll
-                for (int32_t q = 0; q < (int32_t)(RING_WORDS / RING_CHUNK); ++q)
+            for (uint32_t j = 0; j < K; ++j) {
+                if (!(mv & (1u << j))) continue;
+                const int32_t k1 = k1s[j];
+#pragma unroll
+                for (int32_t q = 0; q < (int32_t)NQ; ++q)
                     if (k[j] - q > k1) {
                         const uint32_t slot = (uint32_t)((k[j] - q) * (int32_t)RING_CHUNK + (int32_t)lane) & RING_MASK;
-                        ring_all[j * RING_STRIDE + slot] = v[q];
-                        if (slot == 0u) ring_all[j * RING_STRIDE + RING_WORDS] = v[q];  // the mirror
+                        ring_all[j * RING_STRIDE + slot] = v[j][q];
+                        if (slot == 0u) ring_all[j * RING_STRIDE + RING_WORDS] = v[j][q];  // the mirror
                     }
                 k[j] = k1;
                 if (lane == 0) lds_store_release(&ctl_all[j][0], (k1 + 1) * (int32_t)RING_CHUNK);
                 if (k1 < 0) act &= ~(1u << j);
-                moved = true;
             }
-            if (!moved) __builtin_amdgcn_s_sleep(2);
+            if (!mv) __builtin_amdgcn_s_sleep(2);
         }
         return;
     }
@@ -1379,6 +1409,11 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
     const uint32_t* const ring = ring_all + lane * RING_STRIDE;
     int32_t* const ctl = ctl_all[lane];
     const int32_t info = P.dtinfo[gb];
+    const uint32_t* const dtg = P.dt + gb * (uint64_t)TW;
+    auto sym = [&](uint32_t s) -> uint32_t {  // symbol of state s (end-of-block steps)
+        if constexpr (DEF) return dte_sym(dtg[s]);
+        else return T.symbol(s);
+    };
     const uint8_t* in = P.in + gb * P.slot_bytes;
     const uint32_t clen = info >= 0 ? P.comp_len[gb] : 0u;
     const int32_t nw = (int32_t)((clen + 3u) >> 2);
@@ -1395,7 +1430,9 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
     if (NS == 2 && err == FSE_OK && !known && single) err = FSE_ERR_SINGLE_SYMBOL;
     const int32_t hdr_bits = (info & 0xFFFF) * 8;
     const uint32_t L = (uint32_t)info >> 16;
-    uint32_t o = 0;
+    uint32_t o = 0, o_bulk = 0;
+    // DEF: pair p's states at st_out[p], i.e. 2 bytes per output byte
+    uint32_t* const st_out = DEF ? P.states + gb * (uint64_t)P.block_size / 2u : nullptr;
     int32_t top = 0;
     if (err == FSE_OK) {
         top = (int32_t)(clen - 1u) * 8 + (int32_t)ilog2u(in[clen - 1]);  // marker (BitStackReader::new)
@@ -1442,7 +1479,17 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
             while (o + 18u < lim && c.pos() - hdr_bits >= 16 * (int32_t)L) {
                 wait_words((c.pos() - 32 - 16 * (int32_t)L) >> 5);
                 uint32_t w[4];
-                if constexpr (NS == 2) {
+                if constexpr (DEF) {  // the state pairs, 32 bytes per 8 pairs
+                    uint32_t v[8];
+#pragma unroll
+                    for (uint32_t j = 0; j < 8u; ++j) v[j] = c.pair_states(T);
+                    uint4* sp = reinterpret_cast<uint4*>(st_out + (o >> 1));
+                    sp[0] = make_uint4(v[0], v[1], v[2], v[3]);
+                    sp[1] = make_uint4(v[4], v[5], v[6], v[7]);
+                    o += 16;
+                    lds_store_volatile(&ctl[1], c.pos() >> 5);
+                    continue;
+                } else if constexpr (NS == 2) {
 #pragma unroll
                     for (uint32_t j = 0; j < 8u; j += 2u) {
                         record();
@@ -1471,8 +1518,10 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
                 lds_store_volatile(&ctl[1], c.pos() >> 5);  // the highest word a later step reads
             }
         };
-        if (rec) bulk(std::true_type{});
+        if (DEF) bulk(std::false_type{});  // (never with a sidecar to record)
+        else if (rec) bulk(std::true_type{});
         else bulk(std::false_type{});
+        o_bulk = o;
         // the tail reads words <= pos/32 + 1, and it ends within 16L bits
         // (bulk stopped by the position) or within 18 steps (stopped by the
         // output limit): wait for just those words, the loader cannot pass
@@ -1491,29 +1540,29 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
             for (;; ++pidx) {
                 record_at(pos, s0, s1);
                 if (known && o + 2u >= n) {
-                    if (o < n) out[o++] = (uint8_t)T.symbol(s0);
-                    if (o < n) out[o++] = (uint8_t)T.symbol(s1);
+                    if (o < n) out[o++] = (uint8_t)sym(s0);
+                    if (o < n) out[o++] = (uint8_t)sym(s1);
                     break;
                 }
                 uint32_t nb = T.nb(s0);
                 if (pos - (int32_t)nb < hdr_bits) {  // decoder 0 cannot read: lib.rs:242-243
                     if (o + 2u > lim) { err = full; break; }
-                    out[o++] = (uint8_t)T.symbol(s0);
-                    out[o++] = (uint8_t)T.symbol(s1);
+                    out[o++] = (uint8_t)sym(s0);
+                    out[o++] = (uint8_t)sym(s1);
                     break;
                 }
-                const uint32_t y0 = T.symbol(s0);
+                const uint32_t y0 = sym(s0);
                 s0 = T.next_base(s0) + pop(nb);
                 if (o >= lim) { err = full; break; }
                 out[o++] = (uint8_t)y0;
                 nb = T.nb(s1);
                 if (pos - (int32_t)nb < hdr_bits) {  // decoder 1 cannot read: lib.rs:235-239
                     if (o + 2u > lim) { err = full; break; }
-                    out[o++] = (uint8_t)T.symbol(s1);
-                    out[o++] = (uint8_t)T.symbol(s0);
+                    out[o++] = (uint8_t)sym(s1);
+                    out[o++] = (uint8_t)sym(s0);
                     break;
                 }
-                const uint32_t y1 = T.symbol(s1);
+                const uint32_t y1 = sym(s1);
                 s1 = T.next_base(s1) + pop(nb);
                 if (o >= lim) { err = full; break; }
                 out[o++] = (uint8_t)y1;
@@ -1533,20 +1582,62 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
                     err = single ? FSE_ERR_SINGLE_SYMBOL : FSE_ERR_DST_TOO_SMALL;
                     break;
                 }
-                const uint32_t y = T.symbol(s0);
+                const uint32_t y = sym(s0);
                 s0 = T.next_base(s0) + pop(nb);
                 out[o++] = (uint8_t)y;
             }
             if (err == FSE_OK) {
                 if (o >= lim) err = FSE_ERR_DST_TOO_SMALL;
-                else out[o++] = (uint8_t)T.symbol(s0);  // Decoder::finish (lib.rs:208)
+                else out[o++] = (uint8_t)sym(s0);  // Decoder::finish (lib.rs:208)
             }
             if (known && (err == FSE_ERR_DST_TOO_SMALL || (err == FSE_OK && o != n))) err = FSE_ERR_LENGTH_MISMATCH;
         }
     }
     lds_store_volatile(&ctl[1], INT32_MIN);  // release the loader
+    if (DEF)  // every block, so sym_map_kernel never reads a stale length
+        reinterpret_cast<uint2*>(P.bulk)[gb] = make_uint2(err == FSE_OK ? o_bulk : 0u, T.H & (TW - 1u));
     P.status[gb] = err;
     if (P.out_len) P.out_len[gb] = err ? 0u : o;
+}
+
+// ------------------------------------------------------------------------
+// Deferred symbols (serial_ring_kernel<..., DEF = true>): the chains wrote the
+// state pair of each pair (low 16 bits of the halved entry addresses) instead
+// of its two symbols, so their LDS holds u16 entries only (4 KiB per chain at
+// L <= 11: 8 chains per 37 KB workgroup, 32 per CU instead of 24).  Here one
+// workgroup per block stages the block's symbol column (dte_sym of the
+// prebuilt u32 table) in LDS and maps the bulk's states to bytes: 2 bytes
+// read and 1 written per output byte, fully parallel.  The chains' end-of-
+// block steps wrote their bytes directly, above the bulk length.
+// ------------------------------------------------------------------------
+template <int LMAX>
+__global__ __launch_bounds__(256) void sym_map_kernel(DecParams P) {
+    constexpr uint32_t TW = 1u << LMAX, M = TW - 1u;
+    __shared__ uint8_t sy[TW];
+    const uint64_t gb = blockIdx.x;
+    if (gb >= P.n_blocks) return;
+    const uint2 bk = reinterpret_cast<const uint2*>(P.bulk)[gb];
+    const int32_t info = P.dtinfo[gb];
+    const uint64_t ooff = gb * (uint64_t)P.block_size;
+    const uint32_t lim = P.n_total ? (uint32_t)min((uint64_t)P.block_size, P.n_total - ooff) : P.out_cap;
+    const uint32_t ob = min(bk.x, lim) & ~15u;  // the bulk is whole 16-byte groups
+    if (info < 0 || ob == 0) return;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t nst = 1u << min((uint32_t)info >> 16, (uint32_t)LMAX);
+    const uint32_t* dtg = P.dt + gb * (uint64_t)TW;
+    for (uint32_t i = tid; i < nst; i += 256u) sy[i] = (uint8_t)dte_sym(dtg[i]);
+    __syncthreads();
+    const uint32_t h = bk.y;
+    auto two = [&](uint32_t w) { return (uint32_t)sy[(w - h) & M] | ((uint32_t)sy[((w >> 16) - h) & M] << 8); };
+    const uint4* src = reinterpret_cast<const uint4*>(P.states + ooff / 2u);
+    uint4* dst = reinterpret_cast<uint4*>(P.out + ooff);
+    const uint32_t ng = ob >> 4;  // 16 output bytes = 8 pairs = 2 x uint4 of states
+#pragma unroll 2
+    for (uint32_t i = tid; i < ng; i += 256u) {
+        const uint4 a = src[2u * i], b = src[2u * i + 1u];
+        dst[i] = make_uint4(two(a.x) | (two(a.y) << 16), two(a.z) | (two(a.w) << 16), two(b.x) | (two(b.y) << 16),
+                            two(b.z) | (two(b.w) << 16));
+    }
 }
 
 // ------------------------------------------------------------------------
@@ -1562,6 +1653,10 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
             else if (lmax <= 13) hipLaunchKernelGGL((decode1_serial_kernel<13>), g, dim3(64), 0, stream, P);
             else if (lmax <= 14) hipLaunchKernelGGL((decode1_serial_kernel<14>), g, dim3(64), 0, stream, P);
             else hipLaunchKernelGGL((decode1_serial_kernel<15>), g, dim3(64), 0, stream, P);
+        } else if (lmax <= 11 && P.states && P.bulk && !P.sidecar_out) {
+            // symbols deferred: 8 blocks per workgroup, 32 chains per CU, then the map
+            hipLaunchKernelGGL((serial_ring_kernel<11, 8, 2, true>), dim3((P.n_blocks + 7u) / 8u), dim3(128), 0, stream, P);
+            hipLaunchKernelGGL((sym_map_kernel<11>), dim3(P.n_blocks), dim3(256), 0, stream, P);
         } else {
             // 6 (L <= 11) or 3 (L = 12) blocks per workgroup: 24 / 12 chains per CU (LDS-bound)
             if (lmax <= 11) hipLaunchKernelGGL((serial_ring_kernel<11, 6, 2>), dim3((P.n_blocks + 5u) / 6u), dim3(128), 0, stream, P);
@@ -1652,10 +1747,10 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
 
 int occupancy_report_dec(char* buf, int cap) {
     int len = 0;
-    auto one = [&](const char* name, const void* k) {
+    auto one = [&](const char* name, const void* k, int threads = 256) {
         int nb = -1;
         hipFuncAttributes fa{};
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 256, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, threads, 0);
         (void)hipFuncGetAttributes(&fa, k);
         if (len < cap)
             len += snprintf(buf + len, cap - len, "%s: %d WG/CU (lds %zu B, vgpr %d)\n", name, nb, fa.sharedSizeBytes,
@@ -1664,6 +1759,9 @@ int occupancy_report_dec(char* buf, int cap) {
     one("decode_pre<11,45056,2,1>", reinterpret_cast<const void*>(decode_pre_kernel<11, 45056u, 2, 1>));
     one("decode_pre<11,45056,2,1,512>", reinterpret_cast<const void*>(decode_pre_kernel<11, 45056u, 2, 1, 512>));
     one("decode_pre<11,67584,2,2>", reinterpret_cast<const void*>(decode_pre_kernel<11, 67584u, 2, 2>));
+    one("serial_ring<11,6,2>", reinterpret_cast<const void*>(serial_ring_kernel<11, 6, 2>), 128);
+    one("serial_ring<11,8,2,defer>", reinterpret_cast<const void*>(serial_ring_kernel<11, 8, 2, true>), 128);
+    one("sym_map<11>", reinterpret_cast<const void*>(sym_map_kernel<11>));
     return len;
 }
 

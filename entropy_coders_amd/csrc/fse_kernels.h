@@ -51,6 +51,13 @@ struct DecParams {
     uint32_t pass;          // segment decode: 0 = all blocks, 1 = defer blocks the LDS stage cannot
                             // hold (status FSE_DEFERRED), 2 = only the deferred blocks (list pass)
     uint32_t nstates;       // 2 = fse_compress2 blocks (default), 1 = fse_compress blocks
+    // Sidecar-less 2-state decode at L <= 11 with symbols deferred (optional
+    // workspace; nullptr -> the single-kernel serial decode): the chains write
+    // their state pairs here ([n_blocks][block_size / 2] u32, 2 bytes per
+    // output byte) and the bulk length | table base per block (uint2), and a
+    // map kernel turns the states into symbols.
+    uint32_t* states;
+    uint32_t* bulk;
 };
 
 // Decode-table build (header parse + DecodeTable) for a batch of blocks.

@@ -288,8 +288,12 @@ int fsehip_compress_blocks(const fsehip_params* p, const uint8_t* d_src, uint64_
 /* Decompress blocks produced as above.  With d_sidecar the blocks decode in
  * parallel segments; without it (any valid fse_compress2 stream, e.g. from
  * the CPU crate) each block decodes serially, many at once (one lane per
- * block, its table compact in LDS: 6 blocks per workgroup, 24 chains per
- * CU at table log <= 11).  n_total (> 0) gives the raw length.  slot_bytes
+ * block, its table compact in LDS).  2-state blocks at table log <= 11 keep
+ * only the u16 table entries in LDS (8 blocks per workgroup, 32 chains per
+ * CU) and defer their symbols: the chains write state pairs into the
+ * stream's workspace (2 bytes per output byte) and a map kernel turns them
+ * into bytes; if that workspace cannot be allocated, the single-kernel
+ * decode runs (6 blocks per workgroup, 24 chains per CU).  n_total (> 0) gives the raw length.  slot_bytes
  * is a multiple of 256 (encoder slots are), d_in and d_out 16-byte aligned
  * (BAD_ARG otherwise). */
 int fsehip_decompress_blocks(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
@@ -332,7 +336,9 @@ int fsehip_build_sidecar(const fsehip_params* p, const uint8_t* d_in, uint64_t s
  * the kernels' bound or a stream above 2^28 bytes.  The bound is
  * max_table_log (0 = 11; below 11 it is 11: the smallest kernel variant);
  * the decode-table workspace is 4 << bound bytes per stream (8 KiB at 11,
- * 16 KiB at 12, 32 / 64 / 128 KiB at 13 / 14 / 15).
+ * 16 KiB at 12, 32 / 64 / 128 KiB at 13 / 14 / 15), plus 2 * out_stride + 8
+ * bytes per stream for the deferred symbols of 2-state streams at bound 11
+ * (fsehip_decompress_blocks above).
  * out_stride must be a multiple of 16 and d_out 16-byte aligned (the decoder
  * stores 16-byte groups; BAD_ARG otherwise).
  * Serial per stream, many streams at once. */

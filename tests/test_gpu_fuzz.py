@@ -219,3 +219,44 @@ def _streams_case(nstates, seed, draw):
                 assert g == e.code, (i, mtl, e.code, g)
                 continue
             assert g == want, (i, mtl)
+
+
+@pytest.mark.parametrize("defer", ["1", "0"])
+def test_serial_deferred_symbols(torch_cuda, defer, monkeypatch):
+    """The sidecar-less 2-state decode at L <= 11 with its symbols deferred to
+    sym_map_kernel (the default: state pairs in the workspace, then the map)
+    and without (FSEHIP_SERIAL_DEFER=0, the single-kernel serial decode): ragged
+    batches of the bench's data at several block sizes decode to the source,
+    and crate streams (the oracle's bytes, some damaged) decode as the oracle's
+    fse_decompress2 within the stride, statuses included."""
+    monkeypatch.setenv("FSEHIP_SERIAL_DEFER", defer)
+    torch = torch_cuda
+    from entropy_coders_amd import BlockCodec, decompress_streams
+
+    rng = np.random.default_rng(0xDEF0)
+    for block in (512, 1040, 20000, 65536):
+        sizes = [block] * int(rng.integers(9, 41)) + [int(rng.integers(2, block + 1))]
+        host = np.concatenate([O.generate(0, float(rng.uniform(0.05, 0.8)), int(rng.integers(1 << 30)), 0, s)
+                               for s in sizes])
+        codec = BlockCodec(block_size=block, ckpt_interval=64)
+        src = torch.from_numpy(host).cuda()
+        cb = codec.compress(src)
+        out, st = codec.decompress(cb, use_sidecar=False)
+        torch.cuda.synchronize()
+        assert int(st.abs().max()) == 0, block
+        assert torch.equal(out[: len(host)], src), block
+    streams = []
+    for i in range(40):
+        comp = bytearray(O.compress2(O.generate(0, float(rng.uniform(0.05, 0.8)), i, 0,
+                                                int(rng.integers(2, 30000))), None)[0])
+        if i % 7 == 3:
+            comp[int(rng.integers(0, len(comp)))] ^= 0x5A
+        streams.append(bytes(comp))
+    got = decompress_streams(streams, 24000, nstates=2, max_table_log=11)
+    for i, (x, g) in enumerate(zip(streams, got)):
+        try:
+            want = O.decompress2(x, 24000)
+        except O.OracleError as e:
+            assert g == e.code, (i, e.code, g)
+            continue
+        assert g == want, i
