@@ -330,6 +330,7 @@ static void defer_symbols(Lease& lease, fsehip::DecParams& P, uint32_t lmax) {
     P.states = static_cast<uint32_t*>(lease.get(SCRATCH_STATES, 2ull * P.n_blocks * P.block_size));
     P.bulk = static_cast<uint32_t*>(lease.get(SCRATCH_BULK, 8ull * P.n_blocks));
     if (!P.states || !P.bulk) P.states = P.bulk = nullptr;
+    if (env_u32("FSEHIP_SERIAL_DW", 1) == 2) P.pass = 7u;  // diagnostics: two decode waves (launch_decode)
 }
 
 // Decode on prebuilt tables (dtable_blocks_kernel at stride kern_lmax):

@@ -1288,11 +1288,13 @@ struct RingChain {
     }
 };
 
-template <int LMAX, uint32_t K, int NS, bool DEF = false>
-__global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
+template <int LMAX, uint32_t K, int NS, bool DEF = false, uint32_t DW = 1>
+__global__ __launch_bounds__(64 * (DW + 1)) void serial_ring_kernel(DecParams P) {
     static_assert(LMAX <= 12, "entry layout ns << 18: e >> 16 is the next entry's byte offset");
     static_assert(K >= 1 && K <= 64, "one decode lane per block");
     static_assert(!DEF || (NS == 2 && LMAX <= 11), "deferred symbols: 2-state, L <= 11");
+    static_assert(K % DW == 0, "DW decode waves of K / DW lanes each");
+    constexpr uint32_t NT = 64u * (DW + 1u), KW = K / DW;
     constexpr uint32_t NBW = LMAX <= 11 ? 5u : 4u;  // nb | newState << NBW fits 16 bits
     constexpr uint32_t TW = 1u << LMAX;
     // u16 entries of the K blocks, then their u8 symbols (DEF: entries only;
@@ -1323,7 +1325,7 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
         uint8_t* tb = tab_all + j * 2u * TW;         // entries
         uint8_t* sb = tab_all + K * 2u * TW + j * TW;  // symbols
         uint32_t nbor = 0;
-        for (uint32_t i = tid; i < nv; i += 128u) {
+        for (uint32_t i = tid; i < nv; i += NT) {
             const uint4 q = t4[i];
             // nb | ns << NBW (ns = e >> 18; bits 16, 17 of e are clear) and the
             // symbols, 4 entries at a time
@@ -1340,7 +1342,7 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
     }
     __syncthreads();
 
-    if (tid >= 64u) {  // wave 1: the loader, for all K rings (wave-uniform control)
+    if (tid >= 64u * DW) {  // the last wave: the loader, for all K rings (wave-uniform control)
         int32_t k[K], nwj[K];
         const uint32_t* wj[K];
         uint32_t act = 0;
@@ -1400,14 +1402,15 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
         }
         return;
     }
-    const uint64_t gb = gb0 + lane;
-    if (lane >= K || gb >= P.n_blocks) return;
+    const uint32_t jc = (tid >> 6) * KW + lane;  // this lane's chain
+    const uint64_t gb = gb0 + jc;
+    if (lane >= KW || gb >= P.n_blocks) return;
 
     // wave 0, lane j < K: the decoder of block gb0 + j
     const uint32_t tab0 = lds_addr(tab_all);  // even (16-byte aligned)
-    const RingTab<NBW> T{(tab0 >> 1) + lane * TW, K * 2u * TW + (tab0 >> 1)};
-    const uint32_t* const ring = ring_all + lane * RING_STRIDE;
-    int32_t* const ctl = ctl_all[lane];
+    const RingTab<NBW> T{(tab0 >> 1) + jc * TW, K * 2u * TW + (tab0 >> 1)};
+    const uint32_t* const ring = ring_all + jc * RING_STRIDE;
+    int32_t* const ctl = ctl_all[jc];
     const int32_t info = P.dtinfo[gb];
     const uint32_t* const dtg = P.dt + gb * (uint64_t)TW;
     auto sym = [&](uint32_t s) -> uint32_t {  // symbol of state s (end-of-block steps)
@@ -1417,7 +1420,7 @@ __global__ __launch_bounds__(128) void serial_ring_kernel(DecParams P) {
     const uint8_t* in = P.in + gb * P.slot_bytes;
     const uint32_t clen = info >= 0 ? P.comp_len[gb] : 0u;
     const int32_t nw = (int32_t)((clen + 3u) >> 2);
-    const bool single = any_nb[lane] == 0u;
+    const bool single = any_nb[jc] == 0u;
     const bool known = P.n_total != 0;
     const uint64_t ooff = gb * (uint64_t)P.block_size;
     const uint32_t n = known ? (uint32_t)min((uint64_t)P.block_size, P.n_total - ooff) : 0u;
@@ -1655,7 +1658,10 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
             else hipLaunchKernelGGL((decode1_serial_kernel<15>), g, dim3(64), 0, stream, P);
         } else if (lmax <= 11 && P.states && P.bulk && !P.sidecar_out) {
             // symbols deferred: 8 blocks per workgroup, 32 chains per CU, then the map
-            hipLaunchKernelGGL((serial_ring_kernel<11, 8, 2, true>), dim3((P.n_blocks + 7u) / 8u), dim3(128), 0, stream, P);
+            if (P.pass == 7u)  // diagnostics (FSEHIP_SERIAL_DW=2): two decode waves of 4 chains (measured slower)
+                hipLaunchKernelGGL((serial_ring_kernel<11, 8, 2, true, 2>), dim3((P.n_blocks + 7u) / 8u), dim3(192), 0, stream, P);
+            else  // the 8 chains in one wave
+                hipLaunchKernelGGL((serial_ring_kernel<11, 8, 2, true>), dim3((P.n_blocks + 7u) / 8u), dim3(128), 0, stream, P);
             hipLaunchKernelGGL((sym_map_kernel<11>), dim3(P.n_blocks), dim3(256), 0, stream, P);
         } else {
             // 6 (L <= 11) or 3 (L = 12) blocks per workgroup: 24 / 12 chains per CU (LDS-bound)
