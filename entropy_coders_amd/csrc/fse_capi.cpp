@@ -321,7 +321,7 @@ int fsehip_compress_blocks(const fsehip_params* p, const uint8_t* d_src, uint64_
     return e == hipSuccess ? FSE_OK : FSE_ERR_HIP;
 }
 
-// Sidecar-less 2-state decode at L <= 11: the chains defer their symbols to
+// Sidecar-less decode at L <= 11 (both formats): the chains defer their symbols to
 // a map kernel when the stream's workspace can hold the state pairs (2 bytes
 // per output byte); without it the single-kernel serial decode runs.
 // FSEHIP_SERIAL_DEFER=0 (diagnostics) always takes the latter.
@@ -377,7 +377,7 @@ static int decompress_impl(const fsehip_params* p, const uint8_t* d_in, uint64_t
     P.sidecar_out = d_sidecar_out;
     P.dt = d_dt;
     P.dtinfo = d_dtinfo;
-    if (lease && !d_sidecar && !d_sidecar_out && ns == 2) defer_symbols(*lease, P, kern_lmax(p->max_table_log));
+    if (lease && !d_sidecar && !d_sidecar_out) defer_symbols(*lease, P, kern_lmax(p->max_table_log));
     P.stamps = g_stamps_dec.get(n_blocks);
     hipError_t e = fsehip::launch_decode(P, kern_lmax(p->max_table_log), static_cast<hipStream_t>(stream));
     if (P.stamps) g_stamps_dec.report("decode", n_blocks, static_cast<hipStream_t>(stream));
@@ -499,7 +499,7 @@ int fsehip_decompress_streams(uint32_t nstates, uint32_t max_table_log, const ui
                               P.out_len = d_out_len;
                               P.dt = dt;
                               P.dtinfo = info;
-                              if (P.nstates == 2) defer_symbols(lease, P, kern_lmax(p.max_table_log));
+                              defer_symbols(lease, P, kern_lmax(p.max_table_log));
                               return fsehip::launch_decode(P, kern_lmax(p.max_table_log),
                                                            static_cast<hipStream_t>(stream)) == hipSuccess
                                          ? (int)FSE_OK

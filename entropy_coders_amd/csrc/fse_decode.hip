@@ -1276,6 +1276,16 @@ struct RingChain {
         B1 = T.H + T.ns(e1) + v1;
         return v;
     }
+    // NS = 1, symbol deferred: advances; returns the state it left (halved address)
+    __device__ __forceinline__ uint32_t step_state(const Tab& T) {
+        const uint32_t e = T.entry_at(B0);
+        const uint32_t b = B0;
+        const uint32_t x = window();
+        const uint32_t n0 = T.nbf(e);
+        p32 -= (int32_t)(n0 & 31u);
+        B0 = T.H + T.ns(e) + __builtin_amdgcn_ubfe(x, 0u - n0, n0);
+        return b;
+    }
     // NS = 1: one symbol; returns it
     __device__ __forceinline__ uint32_t step(const Tab& T) {
         const uint32_t e = T.entry_at(B0);
@@ -1292,7 +1302,7 @@ template <int LMAX, uint32_t K, int NS, bool DEF = false, uint32_t DW = 1>
 __global__ __launch_bounds__(64 * (DW + 1)) void serial_ring_kernel(DecParams P) {
     static_assert(LMAX <= 12, "entry layout ns << 18: e >> 16 is the next entry's byte offset");
     static_assert(K >= 1 && K <= 64, "one decode lane per block");
-    static_assert(!DEF || (NS == 2 && LMAX <= 11), "deferred symbols: 2-state, L <= 11");
+    static_assert(!DEF || LMAX <= 11, "deferred symbols: L <= 11");
     static_assert(K % DW == 0, "DW decode waves of K / DW lanes each");
     constexpr uint32_t NT = 64u * (DW + 1u), KW = K / DW;
     constexpr uint32_t NBW = LMAX <= 11 ? 5u : 4u;  // nb | newState << NBW fits 16 bits
@@ -1482,10 +1492,17 @@ __global__ __launch_bounds__(64 * (DW + 1)) void serial_ring_kernel(DecParams P)
             while (o + 18u < lim && c.pos() - hdr_bits >= 16 * (int32_t)L) {
                 wait_words((c.pos() - 32 - 16 * (int32_t)L) >> 5);
                 uint32_t w[4];
-                if constexpr (DEF) {  // the state pairs, 32 bytes per 8 pairs
+                if constexpr (DEF) {  // the states of 16 symbols, 32 bytes per 16 output bytes
                     uint32_t v[8];
 #pragma unroll
-                    for (uint32_t j = 0; j < 8u; ++j) v[j] = c.pair_states(T);
+                    for (uint32_t j = 0; j < 8u; ++j) {
+                        if constexpr (NS == 2) {
+                            v[j] = c.pair_states(T);
+                        } else {
+                            const uint32_t a = c.step_state(T);
+                            v[j] = __builtin_amdgcn_perm(c.step_state(T), a, 0x05040100u);
+                        }
+                    }
                     uint4* sp = reinterpret_cast<uint4*>(st_out + (o >> 1));
                     sp[0] = make_uint4(v[0], v[1], v[2], v[3]);
                     sp[1] = make_uint4(v[4], v[5], v[6], v[7]);
@@ -1651,7 +1668,10 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
     if (!P.dt || !P.dtinfo) return hipErrorInvalidValue;
     if (!P.sidecar) {  // serial: sidecar-less blocks, reference-mode host streams, sidecar recording
         if (P.nstates == 1) {
-            if (lmax <= 11) hipLaunchKernelGGL((serial_ring_kernel<11, 6, 1>), dim3((P.n_blocks + 5u) / 6u), dim3(128), 0, stream, P);
+            if (lmax <= 11 && P.states && P.bulk && !P.sidecar_out) {  // symbols deferred, as below
+                hipLaunchKernelGGL((serial_ring_kernel<11, 8, 1, true>), dim3((P.n_blocks + 7u) / 8u), dim3(128), 0, stream, P);
+                hipLaunchKernelGGL((sym_map_kernel<11>), dim3(P.n_blocks), dim3(256), 0, stream, P);
+            } else if (lmax <= 11) hipLaunchKernelGGL((serial_ring_kernel<11, 6, 1>), dim3((P.n_blocks + 5u) / 6u), dim3(128), 0, stream, P);
             else if (lmax <= 12) hipLaunchKernelGGL((serial_ring_kernel<12, 3, 1>), dim3((P.n_blocks + 2u) / 3u), dim3(128), 0, stream, P);
             else if (lmax <= 13) hipLaunchKernelGGL((decode1_serial_kernel<13>), g, dim3(64), 0, stream, P);
             else if (lmax <= 14) hipLaunchKernelGGL((decode1_serial_kernel<14>), g, dim3(64), 0, stream, P);

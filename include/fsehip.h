@@ -288,7 +288,7 @@ int fsehip_compress_blocks(const fsehip_params* p, const uint8_t* d_src, uint64_
 /* Decompress blocks produced as above.  With d_sidecar the blocks decode in
  * parallel segments; without it (any valid fse_compress2 stream, e.g. from
  * the CPU crate) each block decodes serially, many at once (one lane per
- * block, its table compact in LDS).  2-state blocks at table log <= 11 keep
+ * block, its table compact in LDS).  Blocks at table log <= 11 (both formats) keep
  * only the u16 table entries in LDS (8 blocks per workgroup, 32 chains per
  * CU) and defer their symbols: the chains write state pairs into the
  * stream's workspace (2 bytes per output byte) and a map kernel turns them
@@ -337,7 +337,7 @@ int fsehip_build_sidecar(const fsehip_params* p, const uint8_t* d_in, uint64_t s
  * max_table_log (0 = 11; below 11 it is 11: the smallest kernel variant);
  * the decode-table workspace is 4 << bound bytes per stream (8 KiB at 11,
  * 16 KiB at 12, 32 / 64 / 128 KiB at 13 / 14 / 15), plus 2 * out_stride + 8
- * bytes per stream for the deferred symbols of 2-state streams at bound 11
+ * bytes per stream for the deferred symbols of streams at bound 11
  * (fsehip_decompress_blocks above).
  * out_stride must be a multiple of 16 and d_out 16-byte aligned (the decoder
  * stores 16-byte groups; BAD_ARG otherwise).
