@@ -122,6 +122,59 @@ def host_cpu() -> dict:
     return {"nproc": n_aff, "cgroup_cpu_quota": quota, "usable_cores": usable, "model": model}
 
 
+EXIT_STEP_UNVERIFIED = 3  # the timed step (or a verified side line) failed its check
+EXIT_EXCHANGE_FAILED = 4  # the step verified, the C4 exchange failed or timed out
+
+
+class ExchangeGuard:
+    """Watchdog around the C4 exchange (collectives that may never complete).
+
+    `on_timeout()` runs on the timer thread if `timeout` seconds pass before
+    `finish()`: it prints what the rank has to say and returns the exit code,
+    and the process ends with it (os._exit: a rank blocked in a collective
+    cannot be unwound).  One lock and a done flag make the two outcomes
+    exclusive: once `finish()` has run, a late timer does nothing; once the
+    timer has begun, `finish()` blocks until the process is gone, so no
+    second line is printed."""
+
+    def __init__(self, timeout: float, on_timeout):
+        self._lock = threading.Lock()
+        self._done = False
+        self._on_timeout = on_timeout
+        self._timer = threading.Timer(timeout, self._fire)
+        self._timer.daemon = True
+
+    def _fire(self) -> None:
+        with self._lock:
+            if self._done:
+                return
+            self._done = True
+            code = EXIT_EXCHANGE_FAILED
+            try:
+                code = self._on_timeout()
+            finally:
+                sys.stdout.flush()
+                sys.stderr.flush()
+                os._exit(code)
+
+    def start(self) -> "ExchangeGuard":
+        self._timer.start()
+        return self
+
+    def finish(self) -> None:
+        with self._lock:
+            self._done = True
+        self._timer.cancel()
+
+
+def forced_exchange_failure() -> str | None:
+    """Test hook (tests/test_gpu_dist.py, tests/test_dist_gloo.py): FSEHIP_BENCH_FAIL_EXCHANGE
+    = "raise" makes every rank's exchange raise, "hang" makes rank 1 never
+    reach it (rank 0 then waits in a collective until the watchdog fires)."""
+    v = os.environ.get("FSEHIP_BENCH_FAIL_EXCHANGE", "")
+    return v if v in ("raise", "hang") else None
+
+
 def workload_name(args, n: int) -> str:
     fmt = "fse_compress2" if args.nstates == 2 else "fse_compress"
     gen = {0: "LUT", 1: "geometric", 2: "uniform"}.get(args.kind, f"kind {args.kind}")
@@ -490,23 +543,31 @@ def main():
         return line
 
     gather_info = None
+    exchange_failed = False
     if world > 1 and not args.no_gather:
         # A collective that never completes would hold every rank, and the step's
         # line with them: past --gather-timeout each rank ends itself (os._exit
         # from a timer thread; the collectives release the GIL while they wait),
         # rank 0 after printing the line with the exchange marked timed out.
-        def give_up():
+        # Either way a failed exchange ends the run with EXIT_EXCHANGE_FAILED
+        # (the step's own line still printed), so it is never read as clean.
+        def give_up() -> int:
             if rank == 0:
                 line = step_line()
                 line["c4_exchange"] = {"error": f"no result within {args.gather_timeout:g} s", "verified": False}
                 print(json.dumps(line), flush=True)
             print(f"rank {rank}: C4 exchange timed out", file=sys.stderr, flush=True)
-            os._exit(0 if ok else 3)
+            return EXIT_EXCHANGE_FAILED if ok else EXIT_STEP_UNVERIFIED
 
-        watchdog = threading.Timer(args.gather_timeout, give_up)
-        watchdog.daemon = True
-        watchdog.start()
+        # ranks other than 0 wait 15 s longer: torch.distributed.run stops the
+        # whole group once any rank exits, so rank 0 goes first with the line
+        guard = ExchangeGuard(args.gather_timeout + (15.0 if rank else 0.0), give_up).start()
         try:
+            forced = forced_exchange_failure()
+            if forced == "raise":
+                raise RuntimeError("forced exchange failure (FSEHIP_BENCH_FAIL_EXCHANGE=raise)")
+            if forced == "hang" and rank == 1:
+                time.sleep(10 * args.gather_timeout + 60)  # never joins: rank 0 waits in its collective
             gather_info = c4_exchange(args, codec, cb, src, world, rank, dev, cdev, backend, barrier)
         except Exception as e:  # reported in the line; the timed step above stands on its own checks
             gather_info = {"error": f"{type(e).__name__}: {e}"[:400], "verified": False}
@@ -520,8 +581,9 @@ def main():
         except Exception as e:
             gather_info["verified"] = False
             gather_info.setdefault("error", f"{type(e).__name__}: {e}"[:400])
-        watchdog.cancel()
+        guard.finish()
         if not gather_info["verified"]:
+            exchange_failed = True
             print(f"rank {rank}: C4 exchange not verified", file=sys.stderr, flush=True)
 
     # the same blocks decoded without their sidecar (the format the
@@ -670,9 +732,17 @@ def main():
             line["cpu_baseline"] = cpu_baseline(src.cpu().numpy(), args.block, args.cpu_seconds)
         print(json.dumps(line), flush=True)
     if world > 1:
+        # every rank stays until rank 0 has printed the line (a rank exiting
+        # non-zero first would make torch.distributed.run stop rank 0)
+        try:
+            barrier()
+        except Exception as e:
+            print(f"rank {rank}: final barrier failed: {type(e).__name__}: {e}"[:300], file=sys.stderr, flush=True)
         dist.destroy_process_group()
     if not ok:
-        sys.exit(3)
+        sys.exit(EXIT_STEP_UNVERIFIED)
+    if exchange_failed:
+        sys.exit(EXIT_EXCHANGE_FAILED)
 
 
 def c4_exchange(args, codec, cb, src, world, rank, dev, cdev, backend, barrier) -> dict:

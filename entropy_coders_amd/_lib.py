@@ -10,9 +10,16 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# FSEHIP_LIB: an alternative in-tree build of the same library (A/B timing
-# of compile-time variants, e.g. libfsehip_alt.so); the product is libfsehip.so.
-LIB_PATH = os.path.join(HERE, os.environ.get("FSEHIP_LIB", "libfsehip.so"))
+# FSEHIP_LIB: an alternative in-tree build of the same library for the
+# diagnostics in tools/ -- libfsehip_diag.so (`make diag`: the environment
+# knobs compiled in) or an A/B variant libfsehip_NAME.so
+# (tools/variant_build.sh).  Only a bare libfsehip_*.so name beside this file
+# is accepted; the product is libfsehip.so, which reads no environment.
+_LIB_NAME = os.environ.get("FSEHIP_LIB", "libfsehip.so")
+if _LIB_NAME != "libfsehip.so" and not (
+        _LIB_NAME.startswith("libfsehip_") and _LIB_NAME.endswith(".so") and os.sep not in _LIB_NAME):
+    raise RuntimeError(f"FSEHIP_LIB={_LIB_NAME!r}: expected libfsehip_NAME.so (an in-tree variant build)")
+LIB_PATH = os.path.join(HERE, _LIB_NAME)
 
 # every symbol include/fsehip.h declares (checked by tests/test_abi.py)
 EXPORTS = (
@@ -23,7 +30,7 @@ EXPORTS = (
     "fsehip_pack_blocks", "fsehip_unpack_blocks",
     "fsehip_dtable_bytes", "fsehip_build_dtables", "fsehip_decompress_blocks_dt",
     "fse_compress", "fse_decompress", "fsehip_sidecar_per_block_ns",
-    "fsehip_copy_blocks",
+    "fsehip_copy_blocks", "fsehip_release_workspace",
     "histogram_new", "histogram_normalize", "histogram_normalize_optimal", "norm_histogram_new",
     "norm_histogram_write", "norm_histogram_read", "encode_table_new", "decode_table_new", "fse_compress_nh",
     "bitstack_write", "bitstack_read", "bitstream_read", "bitstream_read_ops",
@@ -144,6 +151,7 @@ def load() -> C.CDLL:
     lib.fsehip_pack_blocks.argtypes = [P, u64, P, P, u32, P, P]
     lib.fsehip_unpack_blocks.argtypes = [P, P, P, u32, P, u64, P]
     lib.fsehip_copy_blocks.argtypes = [P, P, P, u32, P, P, P]
+    lib.fsehip_release_workspace.argtypes = [C.c_int, P]
     H, NH = C.POINTER(Histogram), C.POINTER(NormHistogram)
     lib.histogram_new.argtypes = [P, sz, H]
     lib.histogram_normalize.argtypes = [H, u32, NH]

@@ -41,6 +41,11 @@ struct Workspace {
     std::mutex mu;
     void* ptr[SCRATCH_KINDS] = {};
     uint64_t bytes[SCRATCH_KINDS] = {};
+    // smallest size whose allocation failed (optional buffers only): later
+    // calls asking for as much or more take their fallback at once instead of
+    // retrying a multi-GiB hipMalloc on every call; cleared by
+    // fsehip_release_workspace
+    uint64_t failed[SCRATCH_KINDS] = {};
 };
 std::mutex g_ws_mu;
 std::vector<std::unique_ptr<Workspace>> g_ws;
@@ -64,9 +69,12 @@ struct Lease {
         }
         lk = std::unique_lock<std::mutex>(ws->mu);
     }
-    void* get(int tag, uint64_t bytes) {
+    // `optional`: the caller has a fallback without the buffer (the
+    // deferred-symbol decode), so a failed size is remembered
+    void* get(int tag, uint64_t bytes, bool optional = false) {
         if (!ws) return nullptr;
         if (ws->bytes[tag] < bytes) {
+            if (optional && ws->failed[tag] && bytes >= ws->failed[tag]) return nullptr;
             if (ws->ptr[tag]) {
                 (void)hipStreamSynchronize(static_cast<hipStream_t>(ws->stream));
                 (void)hipFree(ws->ptr[tag]);
@@ -76,6 +84,7 @@ struct Lease {
             if (hipMalloc(&ws->ptr[tag], bytes) != hipSuccess) {
                 (void)hipGetLastError();  // an optional buffer's failure must not surface in a later launch check
                 ws->ptr[tag] = nullptr;
+                if (optional) ws->failed[tag] = ws->failed[tag] ? std::min(ws->failed[tag], bytes) : bytes;
                 return nullptr;
             }
             ws->bytes[tag] = bytes;
@@ -84,12 +93,53 @@ struct Lease {
     }
 };
 
-// Tuning / ablation knobs (not part of the ABI): FSEHIP_ENC_LANES=32|64,
-// FSEHIP_DEBUG bit mask (see fse_kernels.h).
+// Free every buffer of the matching workspaces (device < 0: all devices;
+// stream is matched as given) after the work enqueued on their streams.
+int release_workspaces(int device, void* stream, bool any_stream) {
+    std::vector<Workspace*> hit;
+    {
+        std::lock_guard<std::mutex> g(g_ws_mu);
+        for (auto& x : g_ws)
+            if ((device < 0 || x->dev == device) && (any_stream || x->stream == stream)) hit.push_back(x.get());
+    }
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    int rc = FSE_OK;
+    for (Workspace* w : hit) {
+        std::lock_guard<std::mutex> lk(w->mu);
+        if (hipSetDevice(w->dev) != hipSuccess) {
+            (void)hipGetLastError();
+            rc = FSE_ERR_HIP;
+            continue;
+        }
+        bool any = false;
+        for (int t = 0; t < SCRATCH_KINDS; ++t) any = any || w->ptr[t];
+        if (any && hipStreamSynchronize(static_cast<hipStream_t>(w->stream)) != hipSuccess) rc = FSE_ERR_HIP;
+        for (int t = 0; t < SCRATCH_KINDS; ++t) {
+            if (w->ptr[t] && hipFree(w->ptr[t]) != hipSuccess) rc = FSE_ERR_HIP;
+            w->ptr[t] = nullptr;
+            w->bytes[t] = 0;
+            w->failed[t] = 0;
+        }
+    }
+    (void)hipSetDevice(prev);
+    return rc;
+}
+
+// Tuning / ablation / diagnostics knobs (FSEHIP_ENC_LANES, FSEHIP_DEBUG,
+// FSEHIP_STAMPS, FSEHIP_SERIAL_*, FSEHIP_*_XLDS; see fse_kernels.h) exist
+// only in the diagnostics build libfsehip_diag.so (make diag, -DFSEHIP_DIAG):
+// several of them change the output on purpose (ablations).  The product
+// libfsehip.so reads no environment variable -- every call's result depends
+// on its arguments alone, as the crate's pure functions do.
+#ifdef FSEHIP_DIAG
 uint32_t env_u32(const char* name, uint32_t dflt) {
     const char* v = getenv(name);
     return v && *v ? (uint32_t)strtoul(v, nullptr, 0) : dflt;
 }
+#else
+uint32_t env_u32(const char*, uint32_t dflt) { return dflt; }
+#endif
 
 // FSEHIP_STAMPS=1: per-workgroup phase stamps, averaged and printed to
 // stderr after the (synchronised) launch.  Diagnostics only.
@@ -183,9 +233,13 @@ struct Staging {
     uint8_t* buf[K] = {};
     size_t cap[K] = {};
     int device = -1;
-    ~Staging() {
-        for (int i = 0; i < K; ++i)
+    ~Staging() { release(); }
+    void release() {
+        for (int i = 0; i < K; ++i) {
             if (buf[i]) (void)hipFree(buf[i]);
+            buf[i] = nullptr;
+            cap[i] = 0;
+        }
     }
     uint8_t* get(int i, size_t bytes) {
         int dev = 0;
@@ -277,7 +331,17 @@ int fsehip_device_count(void) {
     return n;
 }
 
-const char* fsehip_version(void) { return "fsehip 0.1 (gfx950)"; }
+#ifdef FSEHIP_DIAG
+const char* fsehip_version(void) { return "fsehip 0.2 (gfx950, diagnostics build: environment knobs live)"; }
+#else
+const char* fsehip_version(void) { return "fsehip 0.2 (gfx950)"; }
+#endif
+
+int fsehip_release_workspace(int device, fsehip_stream_t stream) {
+    const int rc = release_workspaces(device, stream, false);
+    g_stage.release();
+    return rc;
+}
 
 int fsehip_compress_blocks(const fsehip_params* p, const uint8_t* d_src, uint64_t n_total, uint8_t* d_out,
                            uint64_t slot_bytes, uint32_t* d_comp_len, uint32_t* d_payload_bits, uint64_t* d_sidecar,
@@ -325,10 +389,12 @@ int fsehip_compress_blocks(const fsehip_params* p, const uint8_t* d_src, uint64_
 // a map kernel when the stream's workspace can hold the state pairs (2 bytes
 // per output byte); without it the single-kernel serial decode runs.
 // FSEHIP_SERIAL_DEFER=0 (diagnostics) always takes the latter.
+// The map kernel runs one 256-thread workgroup per block, so batches of
+// 2^24 blocks or more (grid x threads >= 2^32) take the single-kernel decode.
 static void defer_symbols(Lease& lease, fsehip::DecParams& P, uint32_t lmax) {
-    if (lmax > 11 || P.block_size < 2u || !env_u32("FSEHIP_SERIAL_DEFER", 1)) return;
-    P.states = static_cast<uint32_t*>(lease.get(SCRATCH_STATES, 2ull * P.n_blocks * P.block_size));
-    P.bulk = static_cast<uint32_t*>(lease.get(SCRATCH_BULK, 8ull * P.n_blocks));
+    if (lmax > 11 || P.block_size < 2u || P.n_blocks >= (1u << 24) || !env_u32("FSEHIP_SERIAL_DEFER", 1)) return;
+    P.states = static_cast<uint32_t*>(lease.get(SCRATCH_STATES, 2ull * P.n_blocks * P.block_size, true));
+    P.bulk = static_cast<uint32_t*>(lease.get(SCRATCH_BULK, 8ull * P.n_blocks, true));
     if (!P.states || !P.bulk) P.states = P.bulk = nullptr;
     if (env_u32("FSEHIP_SERIAL_DW", 1) == 2) P.pass = 7u;  // diagnostics: two decode waves (launch_decode)
 }

@@ -406,6 +406,15 @@ class BlockCodec:
     def _stream(self):
         return C.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
 
+    def release_workspace(self) -> None:
+        """`fsehip_release_workspace` for this codec's device and torch's
+        current stream: frees the decode workspace (decode tables, and the
+        deferred-symbol states: 2 bytes per output byte of the last
+        sidecar-less batch) after the queued work."""
+        check(self.lib.fsehip_release_workspace(self.device.index if self.device.index is not None else
+                                                self.torch.cuda.current_device(), self._stream()),
+              "fsehip_release_workspace")
+
     def n_blocks(self, n_total: int) -> int:
         return (n_total + self.block_size - 1) // self.block_size
 

@@ -291,11 +291,25 @@ int fsehip_compress_blocks(const fsehip_params* p, const uint8_t* d_src, uint64_
  * block, its table compact in LDS).  Blocks at table log <= 11 (both formats) keep
  * only the u16 table entries in LDS (8 blocks per workgroup, 32 chains per
  * CU) and defer their symbols: the chains write state pairs into the
- * stream's workspace (2 bytes per output byte) and a map kernel turns them
- * into bytes; if that workspace cannot be allocated, the single-kernel
- * decode runs (6 blocks per workgroup, 24 chains per CU).  n_total (> 0) gives the raw length.  slot_bytes
- * is a multiple of 256 (encoder slots are), d_in and d_out 16-byte aligned
- * (BAD_ARG otherwise). */
+ * stream's workspace and a map kernel turns them into bytes; if that
+ * workspace cannot be allocated (or the batch has 2^24 blocks or more), the
+ * single-kernel decode runs (6 blocks per workgroup, 24 chains per CU).
+ * n_total (> 0) gives the raw length.  slot_bytes is a multiple of 256, as
+ * encoder slots are (the decode-table build requires it); d_in and d_out
+ * 16-byte aligned (BAD_ARG otherwise).
+ *
+ * Workspace (device memory owned by the library, one per (device, stream),
+ * grown on demand and kept for reuse until fsehip_release_workspace):
+ *   decode tables  fsehip_dtable_bytes(max_table_log) + 4 bytes per block
+ *                  (every call of fsehip_decompress_blocks / _streams /
+ *                  fsehip_build_sidecar);
+ *   deferred symbols (sidecar-less decode at table log <= 11 only):
+ *                  2 bytes per output byte of the batch's capacity
+ *                  (n_blocks x block_size) + 8 bytes per block -- 2 GiB for a
+ *                  1 GiB batch.  A size that failed to allocate is remembered
+ *                  (later calls of that size or more take the single-kernel
+ *                  decode without retrying) until the next release.
+ * Growing a buffer synchronises the stream before freeing the old one. */
 int fsehip_decompress_blocks(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
                              const uint32_t* d_comp_len, const uint64_t* d_sidecar, uint8_t* d_out,
                              uint64_t n_total, int32_t* d_status, fsehip_stream_t stream);
@@ -310,7 +324,9 @@ uint64_t fsehip_dtable_bytes(uint32_t max_table_log);
 int fsehip_build_dtables(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
                          const uint32_t* d_comp_len, uint32_t n_blocks, uint32_t* d_dtables, int32_t* d_dtinfo,
                          fsehip_stream_t stream);
-/* Decompress with prebuilt tables, with or without the sidecar (as above).
+/* Decompress with prebuilt tables, with or without the sidecar (as above;
+ * here slot_bytes need only be a multiple of 32, the staging loads' chunk).
+ * fsehip_build_dtables requires a multiple of 256.
  * fsehip_decompress_blocks runs fsehip_build_dtables + this into a
  * per-stream workspace. */
 int fsehip_decompress_blocks_dt(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
@@ -337,14 +353,22 @@ int fsehip_build_sidecar(const fsehip_params* p, const uint8_t* d_in, uint64_t s
  * max_table_log (0 = 11; below 11 it is 11: the smallest kernel variant);
  * the decode-table workspace is 4 << bound bytes per stream (8 KiB at 11,
  * 16 KiB at 12, 32 / 64 / 128 KiB at 13 / 14 / 15), plus 2 * out_stride + 8
- * bytes per stream for the deferred symbols of streams at bound 11
- * (fsehip_decompress_blocks above).
+ * bytes per stream for the deferred symbols of streams at bound 11 (sized by
+ * the capacity out_stride, not by the bytes decoded; see the workspace note
+ * at fsehip_decompress_blocks and fsehip_release_workspace).
  * out_stride must be a multiple of 16 and d_out 16-byte aligned (the decoder
  * stores 16-byte groups; BAD_ARG otherwise).
  * Serial per stream, many streams at once. */
 int fsehip_decompress_streams(uint32_t nstates, uint32_t max_table_log, const uint8_t* d_in, uint64_t in_stride,
                               const uint32_t* d_comp_len, uint32_t n_streams, uint8_t* d_out, uint32_t out_stride,
                               uint32_t* d_out_len, int32_t* d_status, fsehip_stream_t stream);
+
+/* Free the workspace of (device, stream) -- device < 0: of every device for
+ * that stream handle -- after the work already enqueued on the stream, plus
+ * the calling thread's staging buffers of the host entry points.  The next
+ * call allocates again.  Call it before destroying a stream the library has
+ * been used on.  Returns FSE_OK, or HIP if a synchronise / free failed. */
+int fsehip_release_workspace(int device, fsehip_stream_t stream);
 
 /* Compact the slot layout into one stream (blocks back to back at the byte
  * offsets d_offsets[b], an exclusive scan of d_comp_len) and back.  Used to

@@ -103,3 +103,31 @@ def test_decoder_alignment_rejected_before_any_gpu_work():
     for d_in, slot, d_out in ((ok, 90880 + 16, ok), (odd, 90880, ok), (ok, 90880, odd)):
         rc = lib.fsehip_decompress_blocks_dt(C.byref(p), d_in, slot, ok, None, ok, ok, d_out, 65536, stat, None)
         assert _lib.STATUS[rc] == "BAD_ARG", (d_in, slot, d_out)
+
+
+def test_product_library_reads_no_environment():
+    """The product libfsehip.so has no environment knobs: it does not import
+    getenv and holds none of the diagnostics variables' names (those live in
+    libfsehip_diag.so, `make diag`).  A drop-in must not change its output
+    because of a variable in the caller's environment (lib.rs:146-248 are
+    pure functions)."""
+    import subprocess
+
+    path = os.path.join(ROOT, "entropy_coders_amd", "libfsehip.so")
+    dyn = subprocess.run(["nm", "-D", path], capture_output=True, text=True, check=True).stdout
+    assert not re.search(r"\bU (secure_)?getenv\b", dyn), "product library imports getenv"
+    blob = open(path, "rb").read()
+    for knob in (b"FSEHIP_DEBUG", b"FSEHIP_ENC_LANES", b"FSEHIP_SERIAL_DEFER", b"FSEHIP_SERIAL_DW",
+                 b"FSEHIP_STAMPS", b"FSEHIP_ENC_XLDS", b"FSEHIP_DT_XLDS"):
+        assert knob not in blob, knob
+
+
+def test_lib_variant_name_is_checked():
+    """FSEHIP_LIB (tools only) accepts nothing but an in-tree libfsehip_*.so name."""
+    import subprocess
+    import sys
+
+    for bad in ("../../tmp/x.so", "/tmp/libfsehip_x.so", "libother.so"):
+        r = subprocess.run([sys.executable, "-c", "import entropy_coders_amd"], cwd=ROOT,
+                           env=dict(os.environ, FSEHIP_LIB=bad, PYTHONPATH=ROOT), capture_output=True, text=True)
+        assert r.returncode != 0 and "FSEHIP_LIB" in r.stderr, bad

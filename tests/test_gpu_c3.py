@@ -18,15 +18,17 @@ BLOCKS = 32768
 BLOCK = 65536
 
 
-@pytest.fixture(scope="module")
-def c3():
+# 64 pairs: the bench's own checkpoint interval (512 segments per block,
+# decoded by the 512-thread decode_pre_kernel); 128: 256-thread workgroups
+@pytest.fixture(scope="module", params=[64, 128])
+def c3(request):
     import torch
 
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from entropy_coders_amd import BlockCodec
 
-    codec = BlockCodec(block_size=BLOCK, ckpt_interval=128)
+    codec = BlockCodec(block_size=BLOCK, ckpt_interval=request.param)
     n = BLOCKS * BLOCK
     src = codec.generate(0, 0.155, 0x5EED0003, n)
     cb = codec.compress(src)
@@ -48,10 +50,16 @@ def test_c3_encode_statuses_and_sampled_bytes(c3):
     sample = sorted(set([0, 1, BLOCKS // 2, BLOCKS - 1] + rng.integers(0, BLOCKS, 28).tolist()))
     host = src.view(BLOCKS, BLOCK)[sample].cpu().numpy()
     bits = cb["payload_bits"].cpu().numpy()
+    side = cb["sidecar"].cpu().numpy().view(np.uint64)
     for i, b in enumerate(sample):
         want, wbits = O.compress2(host[i])
         assert codec.block_bytes(cb, b) == want, b
         assert bits[b] == wbits, b
+        bp, s0, s1 = O.checkpoints2(want, codec.ckpt_interval)
+        mine = side[b * codec.side_per_block: b * codec.side_per_block + len(bp)]
+        assert np.array_equal(mine & 0xFFFFFFFF, bp.astype(np.uint64)), b
+        assert np.array_equal((mine >> 32) & 0xFFFF, s0.astype(np.uint64)), b
+        assert np.array_equal(mine >> 48, s1.astype(np.uint64)), b
 
 
 def test_c3_dtable_info(c3):

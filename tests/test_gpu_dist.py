@@ -125,3 +125,44 @@ def test_rccl_one_rank_encode_gather_scatter_decode(scheme):
         p.kill()
     assert code == 0, code
     assert q.get(timeout=10) is True
+
+
+def _bench_two_ranks(extra_env, tmo="60"):
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, FSEHIP_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1", **extra_env)
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--bytes", str(8 * 65536 + 4321), "--no-cpu", "--gather-timeout", tmo]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=400)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r, lines
+
+
+@pytest.mark.parametrize("mode", ["raise", "hang"])
+def test_bench_two_ranks_exchange_failure_exits_nonzero(mode):
+    """bench.py --gpus 2 end to end (two gloo ranks sharing card 0) with the
+    C4 exchange forced to fail (every rank raises) or to hang (rank 1 never
+    joins, the watchdog ends both ranks): the step's line is still printed
+    once, with c4_exchange.verified false, and the run exits with
+    EXIT_EXCHANGE_FAILED (4), never 0."""
+    import json
+
+    r, lines = _bench_two_ranks({"FSEHIP_BENCH_FAIL_EXCHANGE": mode}, tmo="20")
+    assert r.returncode != 0, (r.stdout[-2000:], r.stderr[-3000:])
+    assert len(lines) == 1, (r.stdout[-2000:], r.stderr[-3000:])
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["verified_roundtrip"] is True
+    assert line["c4_exchange"]["verified"] is False
+
+
+def test_bench_two_ranks_exchange_ok():
+    """The same run without a forced failure: exit 0, one line, exchange verified."""
+    import json
+
+    r, lines = _bench_two_ranks({})
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    assert len(lines) == 1
+    line = json.loads(lines[0])
+    assert line["c4_exchange"]["verified"] is True and line["verified_roundtrip"] is True

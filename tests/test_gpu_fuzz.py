@@ -221,42 +221,63 @@ def _streams_case(nstates, seed, draw):
             assert g == want, (i, mtl)
 
 
-@pytest.mark.parametrize("defer", ["1", "0"])
-def test_serial_deferred_symbols(torch_cuda, defer, monkeypatch):
-    """The sidecar-less 2-state decode at L <= 11 with its symbols deferred to
-    sym_map_kernel (the default: state pairs in the workspace, then the map)
-    and without (FSEHIP_SERIAL_DEFER=0, the single-kernel serial decode): ragged
-    batches of the bench's data at several block sizes decode to the source,
-    and crate streams (the oracle's bytes, some damaged) decode as the oracle's
-    fse_decompress2 within the stride, statuses included."""
-    monkeypatch.setenv("FSEHIP_SERIAL_DEFER", defer)
-    torch = torch_cuda
+def _check_serial(torch, nstates: int) -> None:
+    """Sidecar-less decode of ragged batches (several block sizes, the
+    bench's data at random skews) and of crate streams (the oracle's bytes,
+    some damaged) in the crate's own termination, against the oracle."""
     from entropy_coders_amd import BlockCodec, decompress_streams
 
-    rng = np.random.default_rng(0xDEF0)
+    rng = np.random.default_rng(0xDEF0 + nstates)
     for block in (512, 1040, 20000, 65536):
         sizes = [block] * int(rng.integers(9, 41)) + [int(rng.integers(2, block + 1))]
         host = np.concatenate([O.generate(0, float(rng.uniform(0.05, 0.8)), int(rng.integers(1 << 30)), 0, s)
                                for s in sizes])
-        codec = BlockCodec(block_size=block, ckpt_interval=64)
+        codec = BlockCodec(block_size=block, ckpt_interval=64 * nstates, nstates=nstates)
         src = torch.from_numpy(host).cuda()
         cb = codec.compress(src)
         out, st = codec.decompress(cb, use_sidecar=False)
         torch.cuda.synchronize()
         assert int(st.abs().max()) == 0, block
         assert torch.equal(out[: len(host)], src), block
+    comp_fn = (lambda x: O.compress2(x, None)[0]) if nstates == 2 else (lambda x: O.compress(x)[0])
+    dec_fn = O.decompress2 if nstates == 2 else O.decompress
     streams = []
     for i in range(40):
-        comp = bytearray(O.compress2(O.generate(0, float(rng.uniform(0.05, 0.8)), i, 0,
-                                                int(rng.integers(2, 30000))), None)[0])
+        comp = bytearray(comp_fn(O.generate(0, float(rng.uniform(0.05, 0.8)), i, 0, int(rng.integers(2, 30000)))))
         if i % 7 == 3:
             comp[int(rng.integers(0, len(comp)))] ^= 0x5A
         streams.append(bytes(comp))
-    got = decompress_streams(streams, 24000, nstates=2, max_table_log=11)
+    got = decompress_streams(streams, 24000, nstates=nstates, max_table_log=11)
     for i, (x, g) in enumerate(zip(streams, got)):
         try:
-            want = O.decompress2(x, 24000)
+            want = dec_fn(x, 24000)
         except O.OracleError as e:
             assert g == e.code, (i, e.code, g)
             continue
         assert g == want, i
+
+
+@pytest.mark.parametrize("nstates", [2, 1])
+@pytest.mark.parametrize("defer", ["1", "0"])
+def test_serial_deferred_symbols(torch_cuda, defer, nstates):
+    """Both formats' sidecar-less decode at L <= 11: with the symbols deferred
+    to sym_map_kernel (the product default: state pairs in the workspace,
+    then the map) and with the single-kernel serial decode (the product's
+    fallback when that workspace cannot be allocated), selected in a child
+    process on the diagnostics build (FSEHIP_SERIAL_DEFER=0; the product
+    library reads no environment)."""
+    if defer == "1":
+        _check_serial(torch_cuda, nstates)
+        return
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if not os.path.exists(os.path.join(root, "entropy_coders_amd", "libfsehip_diag.so")):
+        pytest.fail("libfsehip_diag.so missing: build it (make -C entropy_coders_amd diag / __graft_entry__.build())")
+    env = dict(os.environ, FSEHIP_LIB="libfsehip_diag.so", FSEHIP_SERIAL_DEFER="0", PYTHONPATH=root)
+    code = ("import torch, tests.test_gpu_fuzz as t; import entropy_coders_amd._lib as L; "
+            "assert L.LIB_PATH.endswith('libfsehip_diag.so'); "
+            f"t._check_serial(torch, {nstates}); print('child-ok')")
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "child-ok" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])

@@ -144,10 +144,14 @@ def test_batched_small_blocks(torch_cuda):
     _batched_roundtrip(torch_cuda, 0, 0.3, 0, 100 * 4096 + 3, block=4096, ckpt=64)
 
 
-def test_batched_1gib_digest(torch_cuda):
-    """Full C2 size: round trip + per-block equality on a sample of blocks."""
+@pytest.mark.parametrize("ckpt", [64, 512])
+def test_batched_1gib_digest(torch_cuda, ckpt):
+    """Full C2 size: exact round trip (sidecar and sidecar-less routes) +
+    per-block bytes, payload bits and sidecar (= the oracle's checkpoints)
+    on sampled blocks.  ckpt 64 is the bench's own setting (512 segments per
+    block: the 512-thread decode_pre_kernel)."""
     torch = torch_cuda
-    cb = _batched_roundtrip(torch, 0, 0.155, 0, 1 << 30, check_all=False)
+    cb = _batched_roundtrip(torch, 0, 0.155, 0, 1 << 30, check_all=False, ckpt=ckpt)
     ratio = float(cb["comp_len"].double().sum()) / (1 << 30)
     assert 0.49 < ratio < 0.52
 

@@ -11,6 +11,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+# the environment knobs this tool sets live only in the diagnostics build
+os.environ.setdefault("FSEHIP_LIB", "libfsehip_diag.so")
 import torch  # noqa: E402
 
 from entropy_coders_amd import BlockCodec  # noqa: E402
