@@ -63,7 +63,11 @@ def parse():
     ap.add_argument("--no-serial", action="store_true", help="skip the sidecar-less decode line")
     ap.add_argument("--no-onestate", action="store_true", help="skip the 1-state format line")
     ap.add_argument("--no-sweep", action="store_true", help="skip the C5 distribution / table-log sweep")
-    ap.add_argument("--sweep-bytes", type=int, default=256 << 20, help="raw bytes per C5 sweep point")
+    ap.add_argument("--no-host-calls", action="store_true",
+                    help="skip the per-call latency of the host fse_compress2 / fse_decompress2 drop-ins")
+    ap.add_argument("--sweep-bytes", type=int, default=1 << 30,
+                    help="raw bytes per C5 sweep point (the step's 1 GiB: at 256 MiB = 4096 blocks over ~2300 "
+                         "resident encode slots the last partial round of slow skewed blocks dominated)")
     ap.add_argument("--host", action="store_true",
                     help="also time the host-streaming pipeline (pinned host buffers, PCIe copies overlapped "
                          "with the kernels); reported separately, never in value")
@@ -286,6 +290,39 @@ def cpu_baseline(src_host: np.ndarray, block: int, budget_s: float) -> dict:
     }
 
 
+def host_call_latency(reps: int = 20) -> dict:
+    """Per-call latency of the reference-shaped host entry points (lib.rs:112-248
+    drop-ins: one 64 KiB C2 block per call, host buffers, PCIe copies and the
+    kernels inside the call), median of `reps`, beside the oracle (the C
+    restatement of the crate, -O3) on one host core doing the same call."""
+    from entropy_coders_amd import compress, compress2, decompress, decompress2
+    from oracle import oracle as O
+
+    src = O.generate(0, 0.155, 0x5EED0002, 0, 65536)
+    comp2, _ = compress2(src)
+    comp1, _ = compress(src)
+    assert decompress2(comp2) == src.tobytes() and decompress(comp1) == src.tobytes()
+
+    def med_us(fn):
+        fn()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return round(float(np.median(ts)) * 1e6, 1)
+
+    cap = 1 << 17
+    return {"workload": "one 64 KiB C2 block per call (host buffers in and out), median of "
+                        f"{reps} calls; oracle = the C restatement on one host core",
+            "fse_compress2_us": med_us(lambda: compress2(src)),
+            "fse_decompress2_us": med_us(lambda: decompress2(comp2, cap)),
+            "fse_compress_us": med_us(lambda: compress(src)),
+            "fse_decompress_us": med_us(lambda: decompress(comp1, cap)),
+            "oracle_compress2_us": med_us(lambda: O.compress2(src)),
+            "oracle_decompress2_us": med_us(lambda: O.decompress2(comp2, cap))}
+
+
 FSE_ERR_ENCODER_INIT = -17  # include/fse_status.h
 
 C5_SWEEP = [  # BASELINE.json configs[4]: (name, generator kind, LUT p, table log)
@@ -376,6 +413,36 @@ def load_traffic(name: str):
         return int(t["bytes_per_launch"]) if t else None
     except (OSError, ValueError, KeyError, TypeError):
         return None
+
+
+def roofline_lds(kernel: str, ms: float, profiled: bool = True):
+    """LDS-side roofline of a kernel whose launch took `ms` (HIP events, this
+    run): its LDS-array cycles per launch summed over the CUs (rocprofv3
+    SQ_LDS_IDX_ACTIVE, profiles/lds.json from tools/pmc_sq.sh +
+    tools/lds_summary.py, same workload) per CU-cycle of this launch, at the
+    clock measured in the profiled launch, against the LDS's peak of one
+    array cycle per clock (MI355X_MICROARCH.md §LDS).  Conflict cycles are
+    counted in (they occupy the array); `useful_frac` leaves them out."""
+    if not profiled:
+        return None
+    try:
+        with open(os.path.join(ROOT, "profiles", "lds.json")) as f:
+            doc = json.load(f)
+        k = doc["kernels"][kernel]
+    except (OSError, ValueError, KeyError, TypeError):
+        return None
+    clk = k.get("clock_ghz")
+    if not clk:
+        return None
+    cycles = ms * 1e-3 * clk * 1e9 * doc.get("cus", 256)
+    busy = k["lds_array_cycles_per_launch"] / cycles
+    useful = (k["lds_array_cycles_per_launch"] - k["bank_conflict_cycles_per_launch"]) / cycles
+    return {"bound": "lds", "kernel": kernel, "unit": "LDS-array cycles per CU-cycle", "achieved": round(busy, 4),
+            "peak": 1.0, "frac": round(busy, 4), "useful_frac": round(useful, 4),
+            "conflict_share": round(k["bank_conflict_cycles_per_launch"] / max(k["lds_array_cycles_per_launch"], 1), 4),
+            "lds_array_cycles_per_launch": k["lds_array_cycles_per_launch"], "clock_ghz": clk,
+            "source": "profiles/lds.json: rocprofv3 SQ_LDS_IDX_ACTIVE / SQ_LDS_BANK_CONFLICT / GRBM_GUI_ACTIVE per "
+                      "launch (tools/pmc_sq.sh, tools/lds_summary.py); time = this run's HIP events"}
 
 
 def roofline(kernel: str, ms: float, alg_bytes: int, what: str, profiled: bool = True) -> dict:
@@ -531,6 +598,9 @@ def main():
             "roofline": roofline("fse_encode_blocks", enc_ms, enc_bytes, "encode launch, HIP events", prof_cfg),
             "roofline_decode": roofline("fse_decode_blocks", dec_ms, dec_bytes,
                                         "decode-table + decode launches, HIP events", prof_cfg),
+            # the encoder is bound by its LDS (random table gathers, histogram
+            # atomics), not by HBM: its LDS-array occupancy beside the HBM line
+            "roofline_lds": roofline_lds("fse_encode_blocks", enc_ms, prof_cfg),
             "encode_ms": round(enc_ms, 4),
             "decode_ms": round(dec_ms, 4),
             "encode_GiB_s": round(n / (enc_ms * 1e-3) / 2**30, 2),
@@ -730,6 +800,8 @@ def main():
             line["verified_roundtrip"] = ok
         if world == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(src.cpu().numpy(), args.block, args.cpu_seconds)
+        if world == 1 and not args.no_host_calls:
+            line["host_call_latency"] = host_call_latency()
         print(json.dumps(line), flush=True)
     if world > 1:
         # every rank stays until rank 0 has printed the line (a rank exiting

@@ -693,9 +693,29 @@ static int decompress_one(const uint8_t* src, size_t n, uint8_t* dst, size_t dst
     int32_t* info = reinterpret_cast<int32_t*>(d_dt + fsehip_dtable_bytes(mtl));
     int rc = fsehip_build_dtables(&p, d_in, padded, &m->comp_len, 1, dt, info, nullptr);
     if (rc) return rc;
-    rc = decompress_impl(&p, d_in, padded, &m->comp_len, nullptr, d_out, 0, nullptr, &m->status, &m->payload_bits,
-                         (uint32_t)cap64, nullptr, dt, info);
-    if (rc) return rc;
+    if (mtl == 11 && n + 8u <= fsehip::single_stage_bytes()) {
+        // the latency-first single-stream decoder (table in VGPRs, chain on
+        // the scalar unit, payload staged in LDS)
+        fsehip::DecParams P{};
+        P.nstates = nstates;
+        P.in = d_in;
+        P.slot_bytes = padded;
+        P.comp_len = &m->comp_len;
+        P.out = d_out;
+        P.n_total = 0;
+        P.block_size = 0;
+        P.n_blocks = 1;
+        P.out_cap = (uint32_t)cap64;
+        P.status = &m->status;
+        P.out_len = &m->payload_bits;
+        P.dt = dt;
+        P.dtinfo = info;
+        if (fsehip::launch_single(P, 11, nullptr) != hipSuccess) return FSE_ERR_HIP;
+    } else {
+        rc = decompress_impl(&p, d_in, padded, &m->comp_len, nullptr, d_out, 0, nullptr, &m->status, &m->payload_bits,
+                             (uint32_t)cap64, nullptr, dt, info);
+        if (rc) return rc;
+    }
     Meta h{};
     if (hipMemcpy(&h, d_meta, sizeof(Meta), hipMemcpyDeviceToHost) != hipSuccess) return FSE_ERR_HIP;
     if (h.status != FSE_OK) return h.status;

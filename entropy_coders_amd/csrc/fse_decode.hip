@@ -21,6 +21,7 @@
 // the table (128 KiB) leaves no LDS for the image, so those blocks are read
 // through a register window from global memory.
 #include <type_traits>
+#include <utility>
 
 #include "fse_device.hpp"
 #include "fse_kernels.h"
@@ -1661,6 +1662,260 @@ __global__ __launch_bounds__(256) void sym_map_kernel(DecParams P) {
 }
 
 // ------------------------------------------------------------------------
+// One stream, as fast as one serial chain goes: the host fse_decompress2 /
+// fse_decompress (lib.rs:187-248) in the reference's own termination.  A
+// lone 2-state stream is a single dependency chain (no
+// speculative split), so this kernel minimises the latency of one step
+// instead of running many chains per CU:
+//   - one wave; the chain is wave-uniform, so its arithmetic runs on the
+//     scalar unit (SGPRs) and never waits on a VGPR round trip;
+//   - the decode table (prebuilt, dtable_blocks_kernel) sits in VGPRs, 64
+//     entries per register: entry s is register s >> 6 (a uniform movrel
+//     index) of lane s & 63 (v_readlane) -- no LDS latency on the chain;
+//   - the payload is staged in LDS once; the 64-bit window refills a word
+//     at a time from a word read one refill ahead, so the bits are always
+//     there when a pair needs them;
+//   - the bulk runs 32 pairs (64 symbols) between end checks; each step's
+//     table entry is parked in a VGPR lane (v_writelane at a constant lane),
+//     and the 64 lanes then store their entries' symbol bytes at once.
+// Blocks whose payload does not fit the LDS stage take serial_ring_kernel.
+// ------------------------------------------------------------------------
+constexpr uint32_t SINGLE_STAGE_BYTES = 144u << 10;  // payload words staged in LDS (dynamic)
+constexpr int32_t SINGLE_PAD = 3;  // zero words below the payload: the window may reach word -3
+
+// The table in registers: entry of state s (wave-uniform s)
+template <uint32_t NV>
+__device__ __forceinline__ uint32_t vtab_at(const uint32_t (&vt)[NV], uint32_t s) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)vt[(s >> 6) & (NV - 1u)], (int)(s & 63u));
+}
+// f(integral_constant<int, 0>) ... f(integral_constant<int, N - 1>)
+template <class F, int... I>
+__device__ __forceinline__ void unroll_impl(F&& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void unroll(F&& f) {
+    unroll_impl(f, std::make_integer_sequence<int, N>{});
+}
+// v = lane J of `buf` (a constant lane: no index register)
+template <int J>
+__device__ __forceinline__ void park(uint32_t& buf, uint32_t v) {
+    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(buf) : "s"(v), "i"(J));
+}
+
+#ifndef FSEHIP_SINGLE_TAB
+#define FSEHIP_SINGLE_TAB 0  // table lookups: 0 = VGPRs + v_readlane, 1 = scalar loads through the K$
+#endif
+typedef __attribute__((address_space(4))) const uint32_t cst_u32;
+
+template <int LMAX, int NS>
+__global__ __launch_bounds__(64) void single_decode_kernel(DecParams P) {
+    static_assert(LMAX == 11, "table in 32 VGPRs (a 64-register array goes to scratch)");
+    extern __shared__ uint32_t pay[];  // SINGLE_PAD zero words, then payload word i at pay[i + SINGLE_PAD]
+    constexpr uint32_t TW = 1u << LMAX, NV = TW / 64u;
+    const uint32_t lane = threadIdx.x;
+    const uint64_t gb = blockIdx.x;
+    if (gb >= P.n_blocks) return;
+    const int32_t info = P.dtinfo[gb];
+    const uint32_t clen = P.comp_len[gb];
+    int32_t err = info < 0 ? info : FSE_OK;
+    const uint32_t L = err == FSE_OK ? (uint32_t)info >> 16 : 0u;
+    const uint32_t nw = (clen + 3u) >> 2;
+    if (err == FSE_OK && (nw + SINGLE_PAD) * 4u > SINGLE_STAGE_BYTES) err = FSE_ERR_UNSUPPORTED;  // host routes these elsewhere
+    // table into VGPRs; OR of the valid entries' nb: 0 = single-symbol table
+    uint32_t vt[NV];
+    uint32_t nbor = 0;
+    {
+        const uint32_t* dtg = P.dt + gb * (uint64_t)TW;
+        const uint32_t size = 1u << L;
+#pragma unroll
+        for (uint32_t k = 0; k < NV; ++k) {
+            vt[k] = dtg[k * 64u + lane];
+            if (k * 64u + lane < size) nbor |= vt[k] & 0xFFu;
+        }
+    }
+    const bool single = __ballot(nbor != 0u) == 0ull;
+    cst_u32* tabk = (cst_u32*)(P.dt + gb * (uint64_t)TW);
+    auto tab = [&](uint32_t st) -> uint32_t {  // entry of state st (wave-uniform)
+        if (FSEHIP_SINGLE_TAB) return tabk[st];
+        return vtab_at(vt, st);
+    };
+    uint8_t* out = P.out + gb * (uint64_t)P.block_size;
+    const uint32_t cap = P.out_cap;
+    if (err == FSE_OK && single) err = FSE_ERR_SINGLE_SYMBOL;  // the reference never ends such a stream
+    if (err != FSE_OK) {
+        if (lane == 0) {
+            P.status[gb] = err;
+            if (P.out_len) P.out_len[gb] = 0;
+        }
+        return;
+    }
+    {  // stage the payload
+        const uint32_t* in32 = reinterpret_cast<const uint32_t*>(P.in + gb * P.slot_bytes);
+        if (lane < (uint32_t)SINGLE_PAD) pay[lane] = 0u;
+        for (uint32_t i = lane; i < nw; i += 64u) pay[i + SINGLE_PAD] = in32[i];
+        __syncthreads();
+    }
+    const int32_t hdr_bits = (info & 0xFFFF) * 8;
+    auto word = [&](int32_t i) -> uint32_t {  // payload word i >= -SINGLE_PAD, wave-uniform
+        return (uint32_t)__builtin_amdgcn_readfirstlane((int)pay[i + SINGLE_PAD]);
+    };
+    const uint32_t lastw = word((int32_t)((clen - 1u) >> 2));
+    const uint32_t lastb = (lastw >> (8u * ((clen - 1u) & 3u))) & 0xFFu;  // non-zero: checked by the table build
+    int32_t pos = (int32_t)(clen - 1u) * 8 + (int32_t)(31u - (uint32_t)__builtin_clz(lastb));  // the marker
+    // window: bits [base, base + 64) of the stream.  The word below it is
+    // read one refill ahead and left in a VGPR (nxt): it is moved to the
+    // scalar side only at the next refill, so the LDS latency is hidden.
+    // pos never falls below hdr_bits >= 8, so base >= -64 and the pads cover
+    // every word a refill reads.
+    int32_t base = ((pos + 31) & ~31) - 64;
+    uint64_t W = (uint64_t)word(base >> 5) | ((uint64_t)word((base >> 5) + 1) << 32);
+    uint32_t nxt = pay[(base >> 5) - 1 + SINGLE_PAD];
+    auto refill = [&]() {  // keep >= 32 bits below pos in the window
+        if (pos - base < 32) {
+            base -= 32;
+            W = (W << 32) | (uint32_t)__builtin_amdgcn_readfirstlane((int)nxt);
+            nxt = pay[(base >> 5) - 1 + SINGLE_PAD];
+        }
+    };
+    auto pop = [&](uint32_t nb) -> uint32_t {
+        pos -= (int32_t)nb;
+        return (uint32_t)(W >> (uint32_t)(pos - base)) & ((1u << nb) - 1u);
+    };
+    uint32_t o = 0;  // bytes decoded
+    // bulk: 64 symbols per round, their entries parked in lanes 0..63 of eb,
+    // then one byte store per lane
+    uint32_t eb = 0;
+    auto put64 = [&]() {
+        out[o + lane] = (uint8_t)dte_sym(eb);
+        o += 64u;
+    };
+    auto put1 = [&](uint32_t sym) {  // one byte (the checked tail)
+        if (lane == 0) out[o] = (uint8_t)sym;
+        ++o;
+    };
+    const int32_t full = FSE_ERR_DST_TOO_SMALL;
+    if (NS == 2) {
+        if (pos - 2 * (int32_t)L < hdr_bits) {
+            err = FSE_ERR_TOO_SHORT;  // lib.rs:224-225 unwrap
+        } else {
+            uint32_t s0 = pop(L);
+            refill();
+            uint32_t s1 = pop(L);
+            refill();
+            // bulk: rounds of 32 pairs that can neither run out of bits (<= 2L
+            // a pair) nor reach the capacity: no end checks
+            for (;;) {
+                const uint32_t by_bits = (uint32_t)(pos - hdr_bits) / (64u * L);
+                const uint32_t by_cap = cap > o + 66u ? (cap - o - 2u) / 64u : 0u;
+                uint32_t g = min(by_bits, by_cap);
+                if (g == 0u) break;
+                for (; g; --g) {
+                    auto step = [&](auto J) {
+                        constexpr int j = decltype(J)::value;
+                        const uint32_t e0 = tab(s0), e1 = tab(s1);
+                        s0 = Dte<LMAX>::ns(e0) + pop(dte_nb(e0));
+                        s1 = Dte<LMAX>::ns(e1) + pop(dte_nb(e1));
+                        refill();  // a pair takes <= 2L = 22 bits, a refill leaves >= 32
+                        park<2 * j>(eb, e0);
+                        park<2 * j + 1>(eb, e1);
+                    };
+                    unroll<32>(step);
+                    put64();
+                }
+            }
+            // tail: pair by pair with the reference's end checks (lib.rs:227-243)
+            for (;;) {
+                const uint32_t e0 = tab(s0);
+                uint32_t nb = dte_nb(e0);
+                if (pos - (int32_t)nb < hdr_bits) {  // decoder 0 cannot read
+                    if (o + 2u > cap) { err = full; break; }
+                    put1(dte_sym(e0));
+                    put1(dte_sym(tab(s1)));
+                    break;
+                }
+                s0 = Dte<LMAX>::ns(e0) + pop(nb);
+                refill();
+                if (o >= cap) { err = full; break; }
+                put1(dte_sym(e0));
+                const uint32_t e1 = tab(s1);
+                nb = dte_nb(e1);
+                if (pos - (int32_t)nb < hdr_bits) {  // decoder 1 cannot read
+                    if (o + 2u > cap) { err = full; break; }
+                    put1(dte_sym(e1));
+                    put1(dte_sym(tab(s0)));
+                    break;
+                }
+                s1 = Dte<LMAX>::ns(e1) + pop(nb);
+                refill();
+                if (o >= cap) { err = full; break; }
+                put1(dte_sym(e1));
+            }
+        }
+    } else {
+        if (pos - (int32_t)L < hdr_bits) {
+            err = FSE_ERR_TOO_SHORT;  // lib.rs:197 unwrap
+        } else {
+            uint32_t s = pop(L);
+            refill();
+            for (;;) {  // bulk: rounds of 64 symbols, no end checks
+                const uint32_t by_bits = (uint32_t)(pos - hdr_bits) / (64u * L);
+                const uint32_t by_cap = cap > o + 65u ? (cap - o - 1u) / 64u : 0u;
+                uint32_t g = min(by_bits, by_cap);
+                if (g == 0u) break;
+                for (; g; --g) {
+                    auto step = [&](auto J) {
+                        constexpr int j = decltype(J)::value;
+                        const uint32_t e = tab(s);
+                        s = Dte<LMAX>::ns(e) + pop(dte_nb(e));
+                        if (j & 1) refill();  // two symbols take <= 2L = 22 bits
+                        park<j>(eb, e);
+                    };
+                    unroll<64>(step);
+                    put64();
+                }
+            }
+            for (;;) {  // lib.rs:198-207 with the read check, then finish (208)
+                const uint32_t e = tab(s);
+                const uint32_t nb = dte_nb(e);
+                if (pos - (int32_t)nb < hdr_bits) break;
+                if (o >= cap) { err = full; break; }
+                s = Dte<LMAX>::ns(e) + pop(nb);
+                refill();
+                put1(dte_sym(e));
+            }
+            if (err == FSE_OK) {
+                if (o >= cap) err = full;
+                else put1(dte_sym(tab(s)));
+            }
+        }
+    }
+    if (lane == 0) {
+        P.status[gb] = err;
+        if (P.out_len) P.out_len[gb] = err ? 0u : o;
+    }
+}
+
+hipError_t launch_single(const DecParams& P, uint32_t lmax, hipStream_t stream) {
+    if (!P.dt || !P.dtinfo || P.n_total || P.sidecar || P.sidecar_out) return hipErrorInvalidValue;
+    const dim3 g(P.n_blocks), b(64);
+    const size_t lds = SINGLE_STAGE_BYTES;
+    if (lmax > 11) return hipErrorInvalidValue;
+    static const bool attr = [] {  // dynamic LDS above the 64 KiB default
+        bool ok = hipFuncSetAttribute(reinterpret_cast<const void*>(single_decode_kernel<11, 1>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)SINGLE_STAGE_BYTES) == hipSuccess;
+        ok = hipFuncSetAttribute(reinterpret_cast<const void*>(single_decode_kernel<11, 2>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)SINGLE_STAGE_BYTES) == hipSuccess && ok;
+        (void)hipGetLastError();
+        return ok;
+    }();
+    (void)attr;
+    if (P.nstates == 1) hipLaunchKernelGGL((single_decode_kernel<11, 1>), g, b, lds, stream, P);
+    else hipLaunchKernelGGL((single_decode_kernel<11, 2>), g, b, lds, stream, P);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------
 // launch wrappers
 // ------------------------------------------------------------------------
 hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) {
@@ -1740,6 +1995,12 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
             run(decode_pre_kernel<15, 16, 1, 0>, 0, 0);
         }
     } else {
+#ifdef FSEHIP_DEC_WINDOW  // A/B only: every block through the global-memory window reader (table-only LDS)
+        if (lmax <= 11 && wide) {
+            run(decode_pre_kernel<11, 16, 2, 0, 512>, 0, 0, 512);
+            return hipGetLastError();
+        }
+#endif
         if (lmax <= 11 && wide) {
             run(decode_pre_kernel<11, PP, 2, 1, 512>, 1, 0, 512);
             run(decode_pre_kernel<11, PB, 2, 2, 512>, 2, 2, 512);

@@ -121,6 +121,11 @@ hipError_t launch_dtables(const DtParams& P, uint32_t lmax, hipStream_t stream);
 // lmax: 11 (blocks of L <= 11), 12 or 15 (L 13..15); decode tables are laid
 // out at that stride (4 << lmax bytes per block).
 hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream);
+// One stream per workgroup, latency-first (the host fse_decompress2 /
+// fse_decompress): reference mode only (n_total = 0, no sidecar), table logs
+// <= 11, payloads up to single_stage_bytes() - 8 bytes (UNSUPPORTED above).
+hipError_t launch_single(const DecParams& P, uint32_t lmax, hipStream_t stream);
+constexpr uint32_t single_stage_bytes() { return 144u << 10; }
 // Diagnostics: resident workgroups per CU of the main kernels, as text.
 int occupancy_report(char* buf, int cap);
 int occupancy_report_dec(char* buf, int cap);

@@ -908,6 +908,9 @@ __global__ __launch_bounds__(256) void generate_kernel(GenParams G) {
 // ------------------------------------------------------------------------
 // launch wrappers
 // ------------------------------------------------------------------------
+#ifndef FSEHIP_ENC_WGS
+#define FSEHIP_ENC_WGS 11u  // resident encode workgroups per CU at L <= 11 (LDS-padded)
+#endif
 hipError_t launch_encode(const EncParams& P, uint32_t lmax, hipStream_t stream) {
     // 32 lanes per block (two blocks per wave) for L <= 12 when asked for;
     // L 13..15 tables (64 KiB stateTable) run one block per workgroup
@@ -930,7 +933,7 @@ hipError_t launch_encode(const EncParams& P, uint32_t lmax, hipStream_t stream) 
             hipFuncAttributes fa{};
             if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(encode_blocks_kernel<11, 64, 2>)) != hipSuccess)
                 return 0u;
-            const size_t per = (160u << 10) / 11u - 64u;  // LDS per workgroup for 11, less allocation slack
+            const size_t per = (160u << 10) / FSEHIP_ENC_WGS - 64u;  // LDS per workgroup for 11, less allocation slack
             return fa.sharedSizeBytes < per ? (uint32_t)(per - fa.sharedSizeBytes) : 0u;
         }();
         if (lmax <= 11) go(encode_blocks_kernel<11, 64, 2>, pad11);

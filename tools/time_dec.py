@@ -44,6 +44,12 @@ out2 = out[:n2]
 st2 = st[: n2 // 65536]
 dec = timed(lambda: codec.decompress_into(cb2, out2, st2), reps)
 ok2 = bool(torch.equal(out2, src2)) and int(st2.abs().max()) == 0
+# encoder variants: the bytes must be the reference's, not just round-trip
+from oracle import oracle as O  # noqa: E402
+
+host2 = src2.view(-1, 65536)
+bytes_ok = all(codec.block_bytes(cb2, b) == O.compress2(host2[b].cpu().numpy())[0] for b in (0, 1, 777, 16383))
+ok2 = ok2 and bytes_ok
 comp3 = int(cb["comp_len"].to(torch.int64).sum())
 side = blocks * codec.side_per_block * 8
 frac = (comp3 + side + n) / (c3 * 1e-3) / 8e12
