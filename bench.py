@@ -418,7 +418,7 @@ def load_traffic(name: str):
 def roofline_lds(kernel: str, ms: float, profiled: bool = True):
     """LDS-side roofline of a kernel whose launch took `ms` (HIP events, this
     run): its LDS-array cycles per launch summed over the CUs (rocprofv3
-    SQ_LDS_IDX_ACTIVE, profiles/lds.json from tools/pmc_sq.sh +
+    SQ_LDS_IDX_ACTIVE, profiles/lds.json from tools/lds_pass.sh +
     tools/lds_summary.py, same workload) per CU-cycle of this launch, at the
     clock measured in the profiled launch, against the LDS's peak of one
     array cycle per clock (MI355X_MICROARCH.md §LDS).  Conflict cycles are
@@ -442,7 +442,7 @@ def roofline_lds(kernel: str, ms: float, profiled: bool = True):
             "conflict_share": round(k["bank_conflict_cycles_per_launch"] / max(k["lds_array_cycles_per_launch"], 1), 4),
             "lds_array_cycles_per_launch": k["lds_array_cycles_per_launch"], "clock_ghz": clk,
             "source": "profiles/lds.json: rocprofv3 SQ_LDS_IDX_ACTIVE / SQ_LDS_BANK_CONFLICT / GRBM_GUI_ACTIVE per "
-                      "launch (tools/pmc_sq.sh, tools/lds_summary.py); time = this run's HIP events"}
+                      "launch (tools/lds_pass.sh, tools/lds_summary.py); time = this run's HIP events"}
 
 
 def roofline(kernel: str, ms: float, alg_bytes: int, what: str, profiled: bool = True) -> dict:
@@ -712,6 +712,10 @@ def main():
               "roofline": roofline("fse_decode_blocks_c3", c3_ms, c3_bytes,
                                    "decode launches (prebuilt tables), HIP events",
                                    prof_base and args.c3_blocks == 32768),
+              # the same launch priced on the reference format's bytes only
+              # (compressed read + raw written; the sidecar is this port's own)
+              "frac_reference_format_bytes": round((comp3 + n3) / (c3_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+              "roofline_lds": roofline_lds("fse_decode_blocks_c3", c3_ms, prof_base and args.c3_blocks == 32768),
               "verified": c3_ok}
         ok = ok and c3_ok
         del src3, cb3, tabs, out3, st3

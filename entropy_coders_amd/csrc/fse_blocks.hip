@@ -379,6 +379,22 @@ __global__ void bits_read_init(const uint8_t* in, uint64_t n_bytes, uint64_t tot
     if (av < 0) result[0] = 0;
 }
 
+// Host-call return (fse_compress2 / fse_decompress2 etc.): the call's 16-byte
+// result record and min(*len, max) bytes of its output into pinned host
+// memory, in the call's stream, so the host waits once and reads both (no
+// device-to-host copy of the record first to learn the length).
+__global__ __launch_bounds__(256) void host_return_kernel(const uint4* __restrict__ meta, const uint8_t* __restrict__ src,
+                                                          const uint32_t* __restrict__ len, uint4* hmeta,
+                                                          uint8_t* hdst, uint32_t max) {
+    const uint32_t n = min(*len, max);
+    if (threadIdx.x == 0) *hmeta = *meta;
+    const uint32_t nv = n >> 4;
+    const uint4* s4 = reinterpret_cast<const uint4*>(src);
+    uint4* d4 = reinterpret_cast<uint4*>(hdst);
+    for (uint32_t i = threadIdx.x; i < nv; i += blockDim.x) d4[i] = s4[i];
+    for (uint32_t i = (nv << 4) + threadIdx.x; i < n; i += blockDim.x) hdst[i] = src[i];
+}
+
 // ------------------------------------------------------------------------
 // launch wrappers
 // ------------------------------------------------------------------------
@@ -398,6 +414,13 @@ hipError_t launch_hdr_read(const uint8_t* src, uint32_t n, fse_norm_histogram* o
 hipError_t launch_table(const fse_norm_histogram* nh, int enc, fse_encode_table* et, fse_decode_table* dt, int32_t* status,
                         hipStream_t s) {
     hipLaunchKernelGGL(table_kernel, dim3(1), dim3(64), 0, s, nh, enc, et, dt, status);
+    return hipGetLastError();
+}
+
+hipError_t launch_host_return(const void* meta, const uint8_t* src, const uint32_t* len, void* hmeta, uint8_t* hdst,
+                              uint32_t max, hipStream_t s) {
+    hipLaunchKernelGGL(host_return_kernel, dim3(1), dim3(256), 0, s, static_cast<const uint4*>(meta), src, len,
+                       static_cast<uint4*>(hmeta), hdst, max);
     return hipGetLastError();
 }
 

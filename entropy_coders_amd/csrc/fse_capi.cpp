@@ -10,6 +10,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <memory>
 #include <mutex>
 #include <vector>
@@ -208,9 +209,12 @@ struct Stamps {
 Stamps g_stamps_enc, g_stamps_dec, g_stamps_dt;
 
 bool device_ok() {
+    static std::atomic<bool> seen{false};  // devices do not go away: ask the runtime once (~17 us a call)
+    if (seen.load(std::memory_order_relaxed)) return true;
     int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess) return false;
-    return n > 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return false;
+    seen.store(true, std::memory_order_relaxed);
+    return true;
 }
 
 uint32_t lmax_for(const fsehip_params* p) {
@@ -267,6 +271,38 @@ struct Staging {
 };
 thread_local Staging g_stage;
 
+// Pinned host staging for the host-pointer calls (grow-only, per thread):
+// [0] the call's input on its way to the device, [1] its result record and
+// output on the way back.  A pageable hipMemcpy costs ~100 us per call here
+// (profiles/r04/single_stream/), a copy through pinned memory a few.
+constexpr size_t kPinOut = size_t(4) << 20;  // output bytes returned through [1]; the rest by hipMemcpy
+struct PinnedStaging {
+    uint8_t* buf[2] = {};
+    size_t cap[2] = {};
+    ~PinnedStaging() { release(); }
+    void release() {
+        for (int i = 0; i < 2; ++i) {
+            if (buf[i]) (void)hipHostFree(buf[i]);
+            buf[i] = nullptr;
+            cap[i] = 0;
+        }
+    }
+    uint8_t* get(int i, size_t bytes) {
+        if (cap[i] < bytes) {
+            if (buf[i]) (void)hipHostFree(buf[i]);
+            buf[i] = nullptr;
+            cap[i] = 0;
+            void* p = nullptr;
+            const size_t want = round_up(std::max<size_t>(bytes, size_t(64) << 10), 4096);
+            if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) return nullptr;
+            buf[i] = static_cast<uint8_t*>(p);
+            cap[i] = want;
+        }
+        return buf[i];
+    }
+};
+thread_local PinnedStaging g_pin;
+
 struct Meta {
     uint32_t comp_len;
     uint32_t payload_bits;
@@ -284,20 +320,37 @@ int compress_one(const uint8_t* src, size_t n, uint32_t table_log, uint8_t* dst,
     fsehip_params p{(uint32_t)round_up(n, 16), table_log, 0, table_log ? std::max<uint32_t>(table_log, 11) : 11,
                     nstates};
     const uint64_t slot = fsehip_slot_bytes(p.block_size, p.max_table_log);
-    uint8_t* d_src = g_stage.get(0, round_up(n, 16) + 16);
+    const size_t in_bytes = round_up(n, 16);
+    const size_t pin_out = std::min<size_t>(slot, kPinOut);
+    uint8_t* d_src = g_stage.get(0, in_bytes + 16);
     uint8_t* d_out = g_stage.get(1, slot);
     uint8_t* d_meta = g_stage.get(2, sizeof(Meta));
-    if (!d_src || !d_out || !d_meta) return FSE_ERR_HIP;
-    if (hipMemcpy(d_src, src, n, hipMemcpyHostToDevice) != hipSuccess) return FSE_ERR_HIP;
+    uint8_t* h_in = g_pin.get(0, in_bytes);
+    uint8_t* h_ret = g_pin.get(1, 256 + pin_out);
+    if (!d_src || !d_out || !d_meta || !h_in || !h_ret) return FSE_ERR_HIP;
+    memcpy(h_in, src, n);
+    auto fail = [](int rc) {  // nothing may still read or write the pinned buffers
+        (void)hipStreamSynchronize(nullptr);
+        return rc;
+    };
+    if (hipMemcpyAsync(d_src, h_in, in_bytes, hipMemcpyHostToDevice, nullptr) != hipSuccess) return fail(FSE_ERR_HIP);
     Meta* m = reinterpret_cast<Meta*>(d_meta);
     int rc = fsehip_compress_blocks(&p, d_src, n, d_out, slot, &m->comp_len, &m->payload_bits, nullptr,
                                     &m->status, nullptr);
-    if (rc) return rc;
-    Meta h{};
-    if (hipMemcpy(&h, d_meta, sizeof(Meta), hipMemcpyDeviceToHost) != hipSuccess) return FSE_ERR_HIP;
+    if (rc) return fail(rc);
+    if (fsehip::launch_host_return(d_meta, d_out, &m->comp_len, h_ret, h_ret + 256, (uint32_t)pin_out, nullptr) !=
+        hipSuccess)
+        return fail(FSE_ERR_HIP);
+    if (hipStreamSynchronize(nullptr) != hipSuccess) return FSE_ERR_HIP;
+    Meta h;
+    memcpy(&h, h_ret, sizeof h);
     if (h.status != FSE_OK) return h.status;
     if (*dst_len > dst_cap || dst_cap - *dst_len < h.comp_len) return FSE_ERR_DST_TOO_SMALL;
-    if (hipMemcpy(dst + *dst_len, d_out, h.comp_len, hipMemcpyDeviceToHost) != hipSuccess) return FSE_ERR_HIP;
+    const size_t head = std::min<size_t>(h.comp_len, pin_out);
+    memcpy(dst + *dst_len, h_ret + 256, head);
+    if (h.comp_len > head &&
+        hipMemcpy(dst + *dst_len + head, d_out + head, h.comp_len - head, hipMemcpyDeviceToHost) != hipSuccess)
+        return FSE_ERR_HIP;
     *dst_len += h.comp_len;
     if (payload_bits) *payload_bits = h.payload_bits;
     return FSE_OK;
@@ -340,6 +393,7 @@ const char* fsehip_version(void) { return "fsehip 0.2 (gfx950)"; }
 int fsehip_release_workspace(int device, fsehip_stream_t stream) {
     const int rc = release_workspaces(device, stream, false);
     g_stage.release();
+    g_pin.release();
     return rc;
 }
 
@@ -673,29 +727,40 @@ static int decompress_one(const uint8_t* src, size_t n, uint8_t* dst, size_t dst
     if (!device_ok()) return FSE_ERR_NO_DEVICE;
     const uint64_t padded = round_up(n + 16, 256);
     const uint64_t cap64 = std::min<uint64_t>(dst_cap - *dst_len, 0x7FFFFFFFu);
-    uint8_t* d_in = g_stage.get(0, padded);
+    const size_t pin_out = std::min<size_t>(cap64, kPinOut);
+    // one device buffer: the result record (Meta) at 0, the stream at 256
+    uint8_t* d_buf = g_stage.get(0, 256 + padded);
     uint8_t* d_out = g_stage.get(1, std::max<uint64_t>(cap64, 16));
-    uint8_t* d_meta = g_stage.get(2, sizeof(Meta));
     // the header's first field is the table log (histogram.rs:438: read(4) +
     // 5): size the tables and pick the kernels by it (the L <= 11 / 12
     // kernels keep the table in LDS; a bad header fails the parse either way)
     const uint32_t Lh = (uint32_t)(src[0] & 15u) + LOG_MIN_HOST;
     const uint32_t mtl = Lh <= 11u ? 11u : Lh <= 12u ? 12u : 15u;
     uint8_t* d_dt = g_stage.get(3, fsehip_dtable_bytes(mtl) + 16);
-    if (!d_in || !d_out || !d_meta || !d_dt) return FSE_ERR_HIP;
-    if (hipMemset(d_in, 0, padded) != hipSuccess) return FSE_ERR_HIP;
-    if (hipMemcpy(d_in, src, n, hipMemcpyHostToDevice) != hipSuccess) return FSE_ERR_HIP;
-    Meta* m = reinterpret_cast<Meta*>(d_meta);
-    Meta h0{(uint32_t)n, 0, 0, 0};
-    if (hipMemcpy(d_meta, &h0, sizeof(Meta), hipMemcpyHostToDevice) != hipSuccess) return FSE_ERR_HIP;
+    uint8_t* h_in = g_pin.get(0, 256 + padded);
+    uint8_t* h_ret = g_pin.get(1, 256 + pin_out);
+    if (!d_buf || !d_out || !d_dt || !h_in || !h_ret) return FSE_ERR_HIP;
+    // the record and the zero-padded stream go over in one copy
+    const Meta h0{(uint32_t)n, 0, 0, 0};
+    memcpy(h_in, &h0, sizeof h0);
+    memcpy(h_in + 256, src, n);
+    memset(h_in + 256 + n, 0, padded - n);
+    auto fail = [](int rc) {  // nothing may still read or write the pinned buffers
+        (void)hipStreamSynchronize(nullptr);
+        return rc;
+    };
+    if (hipMemcpyAsync(d_buf, h_in, 256 + padded, hipMemcpyHostToDevice, nullptr) != hipSuccess)
+        return fail(FSE_ERR_HIP);
+    uint8_t* d_in = d_buf + 256;
+    Meta* m = reinterpret_cast<Meta*>(d_buf);
     fsehip_params p{0, 0, 0, mtl, nstates};
     uint32_t* dt = reinterpret_cast<uint32_t*>(d_dt);
     int32_t* info = reinterpret_cast<int32_t*>(d_dt + fsehip_dtable_bytes(mtl));
     int rc = fsehip_build_dtables(&p, d_in, padded, &m->comp_len, 1, dt, info, nullptr);
-    if (rc) return rc;
-    if (mtl == 11 && n + 8u <= fsehip::single_stage_bytes()) {
-        // the latency-first single-stream decoder (table in VGPRs, chain on
-        // the scalar unit, payload staged in LDS)
+    if (rc) return fail(rc);
+    if (mtl == 11) {
+        // the latency-first single-stream decoder (chain on the scalar unit,
+        // fused table through the scalar cache, payload streamed by chunks)
         fsehip::DecParams P{};
         P.nstates = nstates;
         P.in = d_in;
@@ -710,17 +775,28 @@ static int decompress_one(const uint8_t* src, size_t n, uint8_t* dst, size_t dst
         P.out_len = &m->payload_bits;
         P.dt = dt;
         P.dtinfo = info;
-        if (fsehip::launch_single(P, 11, nullptr) != hipSuccess) return FSE_ERR_HIP;
+        P.states = reinterpret_cast<uint32_t*>(g_stage.get(6, fsehip::single_ftab_bytes()));  // fused bulk table
+        if (!P.states) return fail(FSE_ERR_HIP);
+        if (fsehip::launch_single(P, 11, nullptr) != hipSuccess) return fail(FSE_ERR_HIP);
     } else {
         rc = decompress_impl(&p, d_in, padded, &m->comp_len, nullptr, d_out, 0, nullptr, &m->status, &m->payload_bits,
                              (uint32_t)cap64, nullptr, dt, info);
-        if (rc) return rc;
+        if (rc) return fail(rc);
     }
-    Meta h{};
-    if (hipMemcpy(&h, d_meta, sizeof(Meta), hipMemcpyDeviceToHost) != hipSuccess) return FSE_ERR_HIP;
+    // payload_bits holds the decoded byte count here (0 on error)
+    if (fsehip::launch_host_return(d_buf, d_out, &m->payload_bits, h_ret, h_ret + 256, (uint32_t)pin_out, nullptr) !=
+        hipSuccess)
+        return fail(FSE_ERR_HIP);
+    if (hipStreamSynchronize(nullptr) != hipSuccess) return FSE_ERR_HIP;
+    Meta h;
+    memcpy(&h, h_ret, sizeof h);
     if (h.status != FSE_OK) return h.status;
     const uint32_t out_len = h.payload_bits;  // decoded byte count
-    if (out_len && hipMemcpy(dst + *dst_len, d_out, out_len, hipMemcpyDeviceToHost) != hipSuccess) return FSE_ERR_HIP;
+    const size_t head = std::min<size_t>(out_len, pin_out);
+    memcpy(dst + *dst_len, h_ret + 256, head);
+    if (out_len > head &&
+        hipMemcpy(dst + *dst_len + head, d_out + head, out_len - head, hipMemcpyDeviceToHost) != hipSuccess)
+        return FSE_ERR_HIP;
     *dst_len += out_len;
     return FSE_OK;
 }

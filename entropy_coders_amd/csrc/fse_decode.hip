@@ -1667,21 +1667,28 @@ __global__ __launch_bounds__(256) void sym_map_kernel(DecParams P) {
 // lone 2-state stream is a single dependency chain (no
 // speculative split), so this kernel minimises the latency of one step
 // instead of running many chains per CU:
-//   - one wave; the chain is wave-uniform, so its arithmetic runs on the
-//     scalar unit (SGPRs) and never waits on a VGPR round trip;
-//   - the decode table (prebuilt, dtable_blocks_kernel) sits in VGPRs, 64
-//     entries per register: entry s is register s >> 6 (a uniform movrel
-//     index) of lane s & 63 (v_readlane) -- no LDS latency on the chain;
-//   - the payload is staged in LDS once; the 64-bit window refills a word
-//     at a time from a word read one refill ahead, so the bits are always
-//     there when a pair needs them;
+//   - one wave; the chain is wave-uniform, so it runs on the scalar unit
+//     (SGPRs) and never waits on a VGPR round trip;
+//   - the bulk reads the table through the scalar cache: fused 64-bit
+//     entries (single_ftab_kernel) whose low word is at once the s_bfe_u64
+//     operand of the state's bits and the window update, both entries of a
+//     pair loaded at an SGPR byte offset and awaited together;
+//   - the payload is read from global memory 64 words at a time (one per
+//     lane), the next chunk in flight while the current one is consumed; the
+//     64-bit window refills from a word taken (v_readlane) one refill ahead,
+//     so neither an LDS nor a memory latency is on the chain, and there is no
+//     staging phase and no size limit;
 //   - the bulk runs 32 pairs (64 symbols) between end checks; each step's
-//     table entry is parked in a VGPR lane (v_writelane at a constant lane),
-//     and the 64 lanes then store their entries' symbol bytes at once.
-// Blocks whose payload does not fit the LDS stage take serial_ring_kernel.
+//     entry is parked in a VGPR lane (v_writelane at a constant lane) while
+//     the next pair's loads are in flight, and the 64 lanes then store their
+//     symbols at once;
+//   - the checked tail and the single-symbol test read the table from VGPRs
+//     (32 registers: entry s is lane s & 63 of register s >> 6).
+// Measured per 64 KiB call (tools/host_latency.py): 3.0-3.6 ms with the
+// table in VGPRs (a dependent v_readlane lookup, ~41 cycles) and the payload
+// staged in LDS; 2.8 ms with plain scalar loads of the u32 entries; 2.1 ms
+// with the fused entries (profiles/r04/single_stream/).
 // ------------------------------------------------------------------------
-constexpr uint32_t SINGLE_STAGE_BYTES = 144u << 10;  // payload words staged in LDS (dynamic)
-constexpr int32_t SINGLE_PAD = 3;  // zero words below the payload: the window may reach word -3
 
 // The table in registers: entry of state s (wave-uniform s)
 template <uint32_t NV>
@@ -1702,92 +1709,173 @@ template <int J>
 __device__ __forceinline__ void park(uint32_t& buf, uint32_t v) {
     asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(buf) : "s"(v), "i"(J));
 }
+// lanes J and J + 1 (one asm block: no wait state between the two)
+template <int J>
+__device__ __forceinline__ void park2(uint32_t& buf, uint32_t a, uint32_t b) {
+    asm volatile(
+        "v_writelane_b32 %0, %1, %3\n\t"
+        "v_writelane_b32 %0, %2, %4"
+        : "+v"(buf)
+        : "s"(a), "s"(b), "i"(J), "i"(J + 1));
+}
 
-#ifndef FSEHIP_SINGLE_TAB
-#define FSEHIP_SINGLE_TAB 0  // table lookups: 0 = VGPRs + v_readlane, 1 = scalar loads through the K$
-#endif
-typedef __attribute__((address_space(4))) const uint32_t cst_u32;
+// Fused entry of one state, shaped for the scalar unit:
+//   lo = nb * 0xFFFF | sym << 24, hi = new_state * 8 (the byte offset of the
+//   next entry before its bits: offset = bits * 8 + hi, one s_lshl3_add).
+// With `av` the window bits below pos, op = av + lo = (nb << 16) | (av - nb)
+// (av >= nb) is at once the s_bfe_u64 operand of the state's bits (offset
+// av - nb, width nb; bits 23.. are ignored) and, masked to 16 bits, the new
+// av.  Built per call into DecParams::states (2 words per entry).
+__global__ __launch_bounds__(256) void single_ftab_kernel(const uint32_t* __restrict__ dt, uint32_t* __restrict__ ft,
+                                                           uint32_t tw) {
+    for (uint32_t i = threadIdx.x; i < tw; i += blockDim.x) {
+        const uint32_t e = dt[i];
+        ft[2u * i] = dte_nb(e) * 0xFFFFu | dte_sym(e) << 24;
+        ft[2u * i + 1u] = Dte<11>::ns(e) << 3;
+    }
+}
+// bits of one fused step: W >> (op & 63) masked to (op >> 16) & 127 bits
+__device__ __forceinline__ uint32_t sbfe64(uint64_t W, uint32_t op) {
+    uint64_t r;
+    asm("s_bfe_u64 %0, %1, %2" : "=s"(r) : "s"(W), "s"(op) : "scc");  // s_bfe writes SCC
+    return (uint32_t)r;
+}
+// One fused step's next offset: bfe(W, op) * 8 + hi, as two scalar
+// instructions in one asm block (the bits go through a fixed register pair:
+// separate asm statements get a wait state between them, and the compiler
+// emits a shift and an add for the second)
+__device__ __forceinline__ uint32_t fstep(uint64_t W, uint32_t op, uint32_t hi) {
+    uint32_t r;
+    asm("s_bfe_u64 s[98:99], %1, %2\n\t"
+        "s_lshl3_add_u32 %0, s98, %3"
+        : "=s"(r)
+        : "s"(W), "s"(op), "s"(hi)
+        : "s98", "s99", "scc");
+    return r;
+}
+// issue the scalar loads of fused entries (byte offsets o0, o1 into ft); the
+// caller waits with fent_wait before using them (the compiler does not track
+// these loads)
+__device__ __forceinline__ void fent_load2(uint64_t ft, uint32_t o0, uint32_t o1, uint64_t& f0, uint64_t& f1) {
+    asm volatile(
+        "s_load_dwordx2 %0, %2, %3\n\t"
+        "s_load_dwordx2 %1, %2, %4"
+        : "=&s"(f0), "=&s"(f1)
+        : "s"(ft), "s"(o0), "s"(o1));
+}
+__device__ __forceinline__ void fent_load1(uint64_t ft, uint32_t o, uint64_t& f) {
+    asm volatile("s_load_dwordx2 %0, %1, %2" : "=&s"(f) : "s"(ft), "s"(o));
+}
+// 1-state: load, park the previous entry a in lane J, wait
+template <int J>
+__device__ __forceinline__ void fent_one(uint64_t ft, uint32_t o, uint64_t& f, uint32_t& buf, uint32_t a) {
+    asm volatile(
+        "s_load_dwordx2 %0, %2, %3\n\t"
+        "v_writelane_b32 %1, %4, %5\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&s"(f), "+v"(buf)
+        : "s"(ft), "s"(o), "s"(a), "i"(J));
+}
+__device__ __forceinline__ void fent_wait(uint64_t& f0, uint64_t& f1) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(f0), "+s"(f1));
+}
+// fent_load2, then the previous pair's entries a, b parked in lanes J, J + 1
+// under the loads' latency, then the wait: one asm block (separate ones get
+// a wait state between them)
+template <int J>
+__device__ __forceinline__ void fent_pair(uint64_t ft, uint32_t o0, uint32_t o1, uint64_t& f0, uint64_t& f1,
+                                          uint32_t& buf, uint32_t a, uint32_t b) {
+    asm volatile(
+        "s_load_dwordx2 %0, %3, %4\n\t"
+        "s_load_dwordx2 %1, %3, %5\n\t"
+        "v_writelane_b32 %2, %6, %8\n\t"
+        "v_writelane_b32 %2, %7, %9\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&s"(f0), "=&s"(f1), "+v"(buf)
+        : "s"(ft), "s"(o0), "s"(o1), "s"(a), "s"(b), "i"(J), "i"(J + 1));
+}
 
-template <int LMAX, int NS>
+template <int NS>
 __global__ __launch_bounds__(64) void single_decode_kernel(DecParams P) {
-    static_assert(LMAX == 11, "table in 32 VGPRs (a 64-register array goes to scratch)");
-    extern __shared__ uint32_t pay[];  // SINGLE_PAD zero words, then payload word i at pay[i + SINGLE_PAD]
-    constexpr uint32_t TW = 1u << LMAX, NV = TW / 64u;
+    constexpr uint32_t LMAX = 11, TW = 1u << LMAX, NV = TW / 64u;
     const uint32_t lane = threadIdx.x;
-    const uint64_t gb = blockIdx.x;
-    if (gb >= P.n_blocks) return;
-    const int32_t info = P.dtinfo[gb];
-    const uint32_t clen = P.comp_len[gb];
+    if (blockIdx.x != 0u) return;  // one stream per launch
+    const int32_t info = P.dtinfo[0];
+    const uint32_t clen = P.comp_len[0];
     int32_t err = info < 0 ? info : FSE_OK;
     const uint32_t L = err == FSE_OK ? (uint32_t)info >> 16 : 0u;
-    const uint32_t nw = (clen + 3u) >> 2;
-    if (err == FSE_OK && (nw + SINGLE_PAD) * 4u > SINGLE_STAGE_BYTES) err = FSE_ERR_UNSUPPORTED;  // host routes these elsewhere
     // table into VGPRs; OR of the valid entries' nb: 0 = single-symbol table
     uint32_t vt[NV];
     uint32_t nbor = 0;
     {
-        const uint32_t* dtg = P.dt + gb * (uint64_t)TW;
         const uint32_t size = 1u << L;
 #pragma unroll
         for (uint32_t k = 0; k < NV; ++k) {
-            vt[k] = dtg[k * 64u + lane];
+            vt[k] = P.dt[k * 64u + lane];
             if (k * 64u + lane < size) nbor |= vt[k] & 0xFFu;
         }
     }
     const bool single = __ballot(nbor != 0u) == 0ull;
-    cst_u32* tabk = (cst_u32*)(P.dt + gb * (uint64_t)TW);
-    auto tab = [&](uint32_t st) -> uint32_t {  // entry of state st (wave-uniform)
-        if (FSEHIP_SINGLE_TAB) return tabk[st];
-        return vtab_at(vt, st);
-    };
-    uint8_t* out = P.out + gb * (uint64_t)P.block_size;
+    uint8_t* out = P.out;
     const uint32_t cap = P.out_cap;
     if (err == FSE_OK && single) err = FSE_ERR_SINGLE_SYMBOL;  // the reference never ends such a stream
     if (err != FSE_OK) {
         if (lane == 0) {
-            P.status[gb] = err;
-            if (P.out_len) P.out_len[gb] = 0;
+            P.status[0] = err;
+            if (P.out_len) P.out_len[0] = 0;
         }
         return;
     }
-    {  // stage the payload
-        const uint32_t* in32 = reinterpret_cast<const uint32_t*>(P.in + gb * P.slot_bytes);
-        if (lane < (uint32_t)SINGLE_PAD) pay[lane] = 0u;
-        for (uint32_t i = lane; i < nw; i += 64u) pay[i + SINGLE_PAD] = in32[i];
-        __syncthreads();
-    }
+    const uint32_t* in32 = reinterpret_cast<const uint32_t*>(P.in);
+    const int32_t last = (int32_t)((clen - 1u) >> 2);  // the payload's last word
+    // 64 payload words from word c on, one per lane.  Words below word 0 are
+    // never consumed (bits below the header are not read), so the index is
+    // only clamped into the buffer: an unconditional load straight into its
+    // register, awaited only when the chunk is used.
+    auto chunk = [&](int32_t c) -> uint32_t { return in32[min(max(c + (int32_t)lane, 0), last)]; };
     const int32_t hdr_bits = (info & 0xFFFF) * 8;
-    auto word = [&](int32_t i) -> uint32_t {  // payload word i >= -SINGLE_PAD, wave-uniform
-        return (uint32_t)__builtin_amdgcn_readfirstlane((int)pay[i + SINGLE_PAD]);
-    };
-    const uint32_t lastw = word((int32_t)((clen - 1u) >> 2));
+    const uint32_t lastw = (uint32_t)__builtin_amdgcn_readfirstlane((int)in32[last]);
     const uint32_t lastb = (lastw >> (8u * ((clen - 1u) & 3u))) & 0xFFu;  // non-zero: checked by the table build
-    int32_t pos = (int32_t)(clen - 1u) * 8 + (int32_t)(31u - (uint32_t)__builtin_clz(lastb));  // the marker
-    // window: bits [base, base + 64) of the stream.  The word below it is
-    // read one refill ahead and left in a VGPR (nxt): it is moved to the
-    // scalar side only at the next refill, so the LDS latency is hidden.
-    // pos never falls below hdr_bits >= 8, so base >= -64 and the pads cover
-    // every word a refill reads.
-    int32_t base = ((pos + 31) & ~31) - 64;
-    uint64_t W = (uint64_t)word(base >> 5) | ((uint64_t)word((base >> 5) + 1) << 32);
-    uint32_t nxt = pay[(base >> 5) - 1 + SINGLE_PAD];
-    auto refill = [&]() {  // keep >= 32 bits below pos in the window
-        if (pos - base < 32) {
-            base -= 32;
-            W = (W << 32) | (uint32_t)__builtin_amdgcn_readfirstlane((int)nxt);
-            nxt = pay[(base >> 5) - 1 + SINGLE_PAD];
+    const int32_t pos0 = (int32_t)(clen - 1u) * 8 + (int32_t)(31u - (uint32_t)__builtin_clz(lastb));  // the marker
+    // window W: bits [base, base + 64) of the stream, base = 32 * (cb + li + 1);
+    // av = pos - base bits below pos.  cur holds words [cb, cb + 64), pre the
+    // 64 below (in flight); nxt = word cb + li, the next one into the window.
+    const int32_t wb = (((pos0 + 31) & ~31) - 64) >> 5;  // the window's low word (>= -2)
+    int32_t cb = wb + 1 - 63;
+    uint32_t cur = chunk(cb);
+    uint32_t pre = chunk(cb - 64);
+    int32_t li = wb - 1 - cb;
+    auto lane_word = [&](int32_t l) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)cur, l); };
+    uint64_t W = (uint64_t)lane_word(wb - cb) | ((uint64_t)lane_word(wb + 1 - cb) << 32);
+    uint32_t nxt = lane_word(li);
+    uint32_t av = (uint32_t)(pos0 - 32 * wb);
+    auto bitpos = [&]() -> int32_t { return 32 * (cb + li + 1) + (int32_t)av; };
+    auto shift_in = [&]() {  // one word into the window (av < 32 before)
+        W = (W << 32) | nxt;
+        av += 32u;
+        if (li == 0) {  // the chunk below becomes current; the next one is requested
+            // the copy first, then the load into the register pre frees (a load
+            // into a temporary would be copied, and awaited, at once)
+            asm volatile("v_mov_b32 %0, %1" : "=&v"(cur) : "v"(pre) : "memory");
+            cb -= 64;
+            pre = chunk(cb - 64);
+            li = 64;
         }
+        --li;
+        nxt = lane_word(li);
+    };
+    auto refill = [&]() {  // keep >= 32 bits below pos in the window
+        if (av < 32u) shift_in();
     };
     auto pop = [&](uint32_t nb) -> uint32_t {
-        pos -= (int32_t)nb;
-        return (uint32_t)(W >> (uint32_t)(pos - base)) & ((1u << nb) - 1u);
+        av -= nb;
+        return (uint32_t)(W >> av) & ((1u << nb) - 1u);
     };
+    const uint64_t ft = (uint64_t)P.states;
     uint32_t o = 0;  // bytes decoded
-    // bulk: 64 symbols per round, their entries parked in lanes 0..63 of eb,
-    // then one byte store per lane
-    uint32_t eb = 0;
-    auto put64 = [&]() {
-        out[o + lane] = (uint8_t)dte_sym(eb);
+    uint32_t eb = 0;  // the round's 64 entries, one per lane
+    auto put64 = [&]() {  // the round's symbols (fused entries: sym in bits 24..31)
+        out[o + lane] = (uint8_t)(eb >> 24);
         o += 64u;
     };
     auto put1 = [&](uint32_t sym) {  // one byte (the checked tail)
@@ -1796,7 +1884,7 @@ __global__ __launch_bounds__(64) void single_decode_kernel(DecParams P) {
     };
     const int32_t full = FSE_ERR_DST_TOO_SMALL;
     if (NS == 2) {
-        if (pos - 2 * (int32_t)L < hdr_bits) {
+        if (bitpos() - 2 * (int32_t)L < hdr_bits) {
             err = FSE_ERR_TOO_SHORT;  // lib.rs:224-225 unwrap
         } else {
             uint32_t s0 = pop(L);
@@ -1806,44 +1894,58 @@ __global__ __launch_bounds__(64) void single_decode_kernel(DecParams P) {
             // bulk: rounds of 32 pairs that can neither run out of bits (<= 2L
             // a pair) nor reach the capacity: no end checks
             for (;;) {
-                const uint32_t by_bits = (uint32_t)(pos - hdr_bits) / (64u * L);
+                const uint32_t by_bits = (uint32_t)(bitpos() - hdr_bits) / (64u * L);
                 const uint32_t by_cap = cap > o + 66u ? (cap - o - 2u) / 64u : 0u;
                 uint32_t g = min(by_bits, by_cap);
                 if (g == 0u) break;
+                uint32_t x0 = s0 << 3, x1 = s1 << 3;  // the states as byte offsets into ft
                 for (; g; --g) {
+                    uint64_t p0 = 0, p1 = 0;  // the previous pair's entries
                     auto step = [&](auto J) {
                         constexpr int j = decltype(J)::value;
-                        const uint32_t e0 = tab(s0), e1 = tab(s1);
-                        s0 = Dte<LMAX>::ns(e0) + pop(dte_nb(e0));
-                        s1 = Dte<LMAX>::ns(e1) + pop(dte_nb(e1));
+                        uint64_t f0, f1;
+                        if (j > 0) {
+                            fent_pair<2 * j - 2>(ft, x0, x1, f0, f1, eb, (uint32_t)p0, (uint32_t)p1);
+                        } else {
+                            fent_load2(ft, x0, x1, f0, f1);
+                            fent_wait(f0, f1);
+                        }
+                        uint32_t op = av + (uint32_t)f0;
+                        x0 = fstep(W, op, (uint32_t)(f0 >> 32));
+                        op = (op & 0xFFFFu) + (uint32_t)f1;
+                        x1 = fstep(W, op, (uint32_t)(f1 >> 32));
+                        av = op & 0xFFFFu;
                         refill();  // a pair takes <= 2L = 22 bits, a refill leaves >= 32
-                        park<2 * j>(eb, e0);
-                        park<2 * j + 1>(eb, e1);
+                        p0 = f0;
+                        p1 = f1;
                     };
                     unroll<32>(step);
+                    park2<62>(eb, (uint32_t)p0, (uint32_t)p1);
                     put64();
                 }
+                s0 = x0 >> 3;
+                s1 = x1 >> 3;
             }
             // tail: pair by pair with the reference's end checks (lib.rs:227-243)
             for (;;) {
-                const uint32_t e0 = tab(s0);
+                const uint32_t e0 = vtab_at(vt, s0);
                 uint32_t nb = dte_nb(e0);
-                if (pos - (int32_t)nb < hdr_bits) {  // decoder 0 cannot read
+                if (bitpos() - (int32_t)nb < hdr_bits) {  // decoder 0 cannot read
                     if (o + 2u > cap) { err = full; break; }
                     put1(dte_sym(e0));
-                    put1(dte_sym(tab(s1)));
+                    put1(dte_sym(vtab_at(vt, s1)));
                     break;
                 }
                 s0 = Dte<LMAX>::ns(e0) + pop(nb);
                 refill();
                 if (o >= cap) { err = full; break; }
                 put1(dte_sym(e0));
-                const uint32_t e1 = tab(s1);
+                const uint32_t e1 = vtab_at(vt, s1);
                 nb = dte_nb(e1);
-                if (pos - (int32_t)nb < hdr_bits) {  // decoder 1 cannot read
+                if (bitpos() - (int32_t)nb < hdr_bits) {  // decoder 1 cannot read
                     if (o + 2u > cap) { err = full; break; }
                     put1(dte_sym(e1));
-                    put1(dte_sym(tab(s0)));
+                    put1(dte_sym(vtab_at(vt, s0)));
                     break;
                 }
                 s1 = Dte<LMAX>::ns(e1) + pop(nb);
@@ -1853,32 +1955,44 @@ __global__ __launch_bounds__(64) void single_decode_kernel(DecParams P) {
             }
         }
     } else {
-        if (pos - (int32_t)L < hdr_bits) {
+        if (bitpos() - (int32_t)L < hdr_bits) {
             err = FSE_ERR_TOO_SHORT;  // lib.rs:197 unwrap
         } else {
             uint32_t s = pop(L);
             refill();
             for (;;) {  // bulk: rounds of 64 symbols, no end checks
-                const uint32_t by_bits = (uint32_t)(pos - hdr_bits) / (64u * L);
+                const uint32_t by_bits = (uint32_t)(bitpos() - hdr_bits) / (64u * L);
                 const uint32_t by_cap = cap > o + 65u ? (cap - o - 1u) / 64u : 0u;
                 uint32_t g = min(by_bits, by_cap);
                 if (g == 0u) break;
+                uint32_t x = s << 3;
                 for (; g; --g) {
+                    uint64_t p = 0, dummy = 0;
                     auto step = [&](auto J) {
                         constexpr int j = decltype(J)::value;
-                        const uint32_t e = tab(s);
-                        s = Dte<LMAX>::ns(e) + pop(dte_nb(e));
+                        uint64_t f;
+                        if (j > 0) {
+                            fent_one<j - 1>(ft, x, f, eb, (uint32_t)p);
+                        } else {
+                            fent_load1(ft, x, f);
+                            fent_wait(f, dummy);
+                        }
+                        const uint32_t op = av + (uint32_t)f;
+                        x = fstep(W, op, (uint32_t)(f >> 32));
+                        av = op & 0xFFFFu;
                         if (j & 1) refill();  // two symbols take <= 2L = 22 bits
-                        park<j>(eb, e);
+                        p = f;
                     };
                     unroll<64>(step);
+                    park<63>(eb, (uint32_t)p);
                     put64();
                 }
+                s = x >> 3;
             }
             for (;;) {  // lib.rs:198-207 with the read check, then finish (208)
-                const uint32_t e = tab(s);
+                const uint32_t e = vtab_at(vt, s);
                 const uint32_t nb = dte_nb(e);
-                if (pos - (int32_t)nb < hdr_bits) break;
+                if (bitpos() - (int32_t)nb < hdr_bits) break;
                 if (o >= cap) { err = full; break; }
                 s = Dte<LMAX>::ns(e) + pop(nb);
                 refill();
@@ -1886,32 +2000,22 @@ __global__ __launch_bounds__(64) void single_decode_kernel(DecParams P) {
             }
             if (err == FSE_OK) {
                 if (o >= cap) err = full;
-                else put1(dte_sym(tab(s)));
+                else put1(dte_sym(vtab_at(vt, s)));
             }
         }
     }
     if (lane == 0) {
-        P.status[gb] = err;
-        if (P.out_len) P.out_len[gb] = err ? 0u : o;
+        P.status[0] = err;
+        if (P.out_len) P.out_len[0] = err ? 0u : o;
     }
 }
 
 hipError_t launch_single(const DecParams& P, uint32_t lmax, hipStream_t stream) {
-    if (!P.dt || !P.dtinfo || P.n_total || P.sidecar || P.sidecar_out) return hipErrorInvalidValue;
-    const dim3 g(P.n_blocks), b(64);
-    const size_t lds = SINGLE_STAGE_BYTES;
-    if (lmax > 11) return hipErrorInvalidValue;
-    static const bool attr = [] {  // dynamic LDS above the 64 KiB default
-        bool ok = hipFuncSetAttribute(reinterpret_cast<const void*>(single_decode_kernel<11, 1>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)SINGLE_STAGE_BYTES) == hipSuccess;
-        ok = hipFuncSetAttribute(reinterpret_cast<const void*>(single_decode_kernel<11, 2>),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)SINGLE_STAGE_BYTES) == hipSuccess && ok;
-        (void)hipGetLastError();
-        return ok;
-    }();
-    (void)attr;
-    if (P.nstates == 1) hipLaunchKernelGGL((single_decode_kernel<11, 1>), g, b, lds, stream, P);
-    else hipLaunchKernelGGL((single_decode_kernel<11, 2>), g, b, lds, stream, P);
+    if (!P.dt || !P.dtinfo || !P.states || P.n_total || P.sidecar || P.sidecar_out || P.n_blocks != 1 || lmax > 11)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(single_ftab_kernel, dim3(1), dim3(256), 0, stream, P.dt, P.states, 2048u);
+    if (P.nstates == 1) hipLaunchKernelGGL((single_decode_kernel<1>), dim3(1), dim3(64), 0, stream, P);
+    else hipLaunchKernelGGL((single_decode_kernel<2>), dim3(1), dim3(64), 0, stream, P);
     return hipGetLastError();
 }
 

@@ -99,6 +99,10 @@ hipError_t launch_hdr_read(const uint8_t* src, uint32_t n, fse_norm_histogram* o
                            hipStream_t s);
 hipError_t launch_table(const fse_norm_histogram* nh, int enc, fse_encode_table* et, fse_decode_table* dt,
                         int32_t* status, hipStream_t s);
+// Host-call return: the 16-byte record at meta and min(*len, max) bytes of
+// src into pinned host memory (hmeta, hdst; 16-byte aligned).
+hipError_t launch_host_return(const void* meta, const uint8_t* src, const uint32_t* len, void* hmeta, uint8_t* hdst,
+                              uint32_t max, hipStream_t s);
 // Bitstream primitives: a tile scan of the field widths (tile_sum: u32 per
 // tile, tile_off: u64 per tile, total: u64), then pack or unpack.
 uint64_t bits_tiles(uint64_t count);
@@ -121,11 +125,12 @@ hipError_t launch_dtables(const DtParams& P, uint32_t lmax, hipStream_t stream);
 // lmax: 11 (blocks of L <= 11), 12 or 15 (L 13..15); decode tables are laid
 // out at that stride (4 << lmax bytes per block).
 hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream);
-// One stream per workgroup, latency-first (the host fse_decompress2 /
-// fse_decompress): reference mode only (n_total = 0, no sidecar), table logs
-// <= 11, payloads up to single_stage_bytes() - 8 bytes (UNSUPPORTED above).
+// One stream, latency-first (the host fse_decompress2 / fse_decompress):
+// reference mode only (n_total = 0, no sidecar, n_blocks = 1), table logs
+// <= 11, any payload length.  P.states: single_ftab_bytes() of device
+// scratch (the fused bulk table).
 hipError_t launch_single(const DecParams& P, uint32_t lmax, hipStream_t stream);
-constexpr uint32_t single_stage_bytes() { return 144u << 10; }
+constexpr uint32_t single_ftab_bytes() { return 2048u * 8u; }
 // Diagnostics: resident workgroups per CU of the main kernels, as text.
 int occupancy_report(char* buf, int cap);
 int occupancy_report_dec(char* buf, int cap);

@@ -7,6 +7,7 @@ compute goes through libfsehip.so on the GPU.
 from __future__ import annotations
 
 import ctypes as C
+import threading
 
 import numpy as np
 
@@ -24,12 +25,26 @@ def _p(a: np.ndarray):
     return a.ctypes.data_as(C.c_void_p)
 
 
+_tls = threading.local()
+
+
+def _out(cap: int) -> np.ndarray:
+    """A per-thread output buffer of >= cap bytes, reused across calls (the
+    calls return copies): allocating a fresh 16 MiB array per call costs
+    more than a small decode."""
+    b = getattr(_tls, "out", None)
+    if b is None or len(b) < cap:
+        b = np.empty(max(cap, 1), dtype=np.uint8)
+        _tls.out = b
+    return b
+
+
 def compress2(src) -> tuple[bytes, int]:
     """`fse_compress2(src, &mut dst) -> usize` (lib.rs:146): (bytes, payload bits)."""
     a = _buf(src)
     lib = load()
     cap = int(lib.fsehip_slot_bytes(max(len(a), 16), 12))
-    dst = np.zeros(cap, dtype=np.uint8)
+    dst = _out(cap)
     n = C.c_size_t(0)
     bits = C.c_uint64(0)
     check(lib.fse_compress2(_p(a), len(a), _p(dst), cap, C.byref(n), C.byref(bits)), "fse_compress2")
@@ -41,7 +56,7 @@ def compress2_log(src, table_log: int) -> tuple[bytes, int]:
     a = _buf(src)
     lib = load()
     cap = int(lib.fsehip_slot_bytes(max(len(a), 16), 12))
-    dst = np.zeros(cap, dtype=np.uint8)
+    dst = _out(cap)
     n = C.c_size_t(0)
     bits = C.c_uint64(0)
     check(lib.fse_compress2_log(_p(a), len(a), table_log, _p(dst), cap, C.byref(n), C.byref(bits)),
@@ -53,7 +68,7 @@ def decompress2(src, cap: int = 1 << 24) -> bytes:
     """`fse_decompress2(src, &mut dst) -> Option<usize>` (lib.rs:215)."""
     a = _buf(src)
     lib = load()
-    dst = np.zeros(max(cap, 1), dtype=np.uint8)
+    dst = _out(cap)
     n = C.c_size_t(0)
     check(lib.fse_decompress2(_p(a), len(a), _p(dst), cap, C.byref(n)), "fse_decompress2")
     return dst[: n.value].tobytes()
@@ -66,7 +81,7 @@ def compress(src) -> tuple[bytes, int]:
     a = _buf(src)
     lib = load()
     cap = int(lib.fsehip_slot_bytes(max(len(a), 16), 12))
-    dst = np.zeros(cap, dtype=np.uint8)
+    dst = _out(cap)
     n = C.c_size_t(0)
     bits = C.c_uint64(0)
     check(lib.fse_compress(_p(a), len(a), _p(dst), cap, C.byref(n), C.byref(bits)), "fse_compress")
@@ -77,7 +92,7 @@ def decompress(src, cap: int = 1 << 24) -> bytes:
     """`fse_decompress(src, &mut dst) -> Option<usize>` (lib.rs:187)."""
     a = _buf(src)
     lib = load()
-    dst = np.zeros(max(cap, 1), dtype=np.uint8)
+    dst = _out(cap)
     n = C.c_size_t(0)
     check(lib.fse_decompress(_p(a), len(a), _p(dst), cap, C.byref(n)), "fse_decompress")
     return dst[: n.value].tobytes()
@@ -194,7 +209,7 @@ def compress_nh(src) -> tuple[bytes, int, NormHistogram]:
     a = _buf(src)
     lib = load()
     cap = int(lib.fsehip_slot_bytes(max(len(a), 16), 12))
-    dst = np.zeros(cap, dtype=np.uint8)
+    dst = _out(cap)
     n = C.c_size_t(0)
     bits = C.c_uint64(0)
     nh = NormHistogram()

@@ -1,5 +1,8 @@
 """Per-call latency of the reference-shaped host entry points (one block
-through PCIe per call) against the oracle on one host core."""
+through PCIe per call) against the oracle on one host core.
+
+    python tools/host_latency.py [SIZE ...]   (default 4096 65536 1048576)
+"""
 import os
 import sys
 import time
@@ -10,7 +13,8 @@ sys.path.insert(0, ROOT)
 from entropy_coders_amd import compress, compress2, decompress, decompress2  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 
-for n in (4096, 65536, 1 << 20):
+SIZES = [int(a) for a in sys.argv[1:]] or [4096, 65536, 1 << 20]
+for n in SIZES:
     src = O.generate(0, 0.155, 0x5EED0002, 0, n)
     comp, _ = compress2(src)
     comp1, _ = compress(src)
