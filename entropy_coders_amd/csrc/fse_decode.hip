@@ -1734,16 +1734,11 @@ __global__ __launch_bounds__(256) void single_ftab_kernel(const uint32_t* __rest
         ft[2u * i + 1u] = Dte<11>::ns(e) << 3;
     }
 }
-// bits of one fused step: W >> (op & 63) masked to (op >> 16) & 127 bits
-__device__ __forceinline__ uint32_t sbfe64(uint64_t W, uint32_t op) {
-    uint64_t r;
-    asm("s_bfe_u64 %0, %1, %2" : "=s"(r) : "s"(W), "s"(op) : "scc");  // s_bfe writes SCC
-    return (uint32_t)r;
-}
-// One fused step's next offset: bfe(W, op) * 8 + hi, as two scalar
-// instructions in one asm block (the bits go through a fixed register pair:
-// separate asm statements get a wait state between them, and the compiler
-// emits a shift and an add for the second)
+// One fused step's next offset: bfe(W, op) * 8 + hi (W >> (op & 63) masked
+// to (op >> 16) & 127 bits), as two scalar instructions in one asm block
+// (the bits go through a fixed register pair: separate asm statements get a
+// wait state between them, and the compiler emits a shift and an add for
+// the second).  s_bfe and s_lshl3_add write SCC.
 __device__ __forceinline__ uint32_t fstep(uint64_t W, uint32_t op, uint32_t hi) {
     uint32_t r;
     asm("s_bfe_u64 s[98:99], %1, %2\n\t"
@@ -1753,46 +1748,50 @@ __device__ __forceinline__ uint32_t fstep(uint64_t W, uint32_t op, uint32_t hi) 
         : "s98", "s99", "scc");
     return r;
 }
-// issue the scalar loads of fused entries (byte offsets o0, o1 into ft); the
-// caller waits with fent_wait before using them (the compiler does not track
-// these loads)
-__device__ __forceinline__ void fent_load2(uint64_t ft, uint32_t o0, uint32_t o1, uint64_t& f0, uint64_t& f1) {
-    asm volatile(
-        "s_load_dwordx2 %0, %2, %3\n\t"
-        "s_load_dwordx2 %1, %2, %4"
-        : "=&s"(f0), "=&s"(f1)
-        : "s"(ft), "s"(o0), "s"(o1));
-}
-__device__ __forceinline__ void fent_load1(uint64_t ft, uint32_t o, uint64_t& f) {
-    asm volatile("s_load_dwordx2 %0, %1, %2" : "=&s"(f) : "s"(ft), "s"(o));
-}
-// 1-state: load, park the previous entry a in lane J, wait
+// The bulk's software pipeline: a step computes its pair's next offsets,
+// issues the scalar loads of those entries (fent_issue*: SGPR byte offsets
+// into ft, no 64-bit address arithmetic) and parks its own entries in VGPR
+// lanes in the same asm block, then refills the window while the loads are
+// in flight; the next step starts with fent_wait*.  The compiler does not
+// track these loads: the registers they write stay live until the wait that
+// names them (so nothing else is put there meanwhile), and `av` is tied to
+// the issue and `W`, `av` to the wait so that the refill stays between them.
 template <int J>
-__device__ __forceinline__ void fent_one(uint64_t ft, uint32_t o, uint64_t& f, uint32_t& buf, uint32_t a) {
+__device__ __forceinline__ void fent_issue2(uint64_t ft, uint32_t o0, uint32_t o1, uint64_t& f0, uint64_t& f1,
+                                            uint32_t& buf, uint32_t a, uint32_t b, uint32_t& av) {
     asm volatile(
-        "s_load_dwordx2 %0, %2, %3\n\t"
-        "v_writelane_b32 %1, %4, %5\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&s"(f), "+v"(buf)
-        : "s"(ft), "s"(o), "s"(a), "i"(J));
+        "s_load_dwordx2 %0, %4, %5\n\t"
+        "s_load_dwordx2 %1, %4, %6\n\t"
+        "v_writelane_b32 %2, %7, %9\n\t"
+        "v_writelane_b32 %2, %8, %10"
+        : "=&s"(f0), "=&s"(f1), "+v"(buf), "+s"(av)
+        : "s"(ft), "s"(o0), "s"(o1), "s"(a), "s"(b), "i"(J), "i"(J + 1));
 }
-__device__ __forceinline__ void fent_wait(uint64_t& f0, uint64_t& f1) {
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(f0), "+s"(f1));
-}
-// fent_load2, then the previous pair's entries a, b parked in lanes J, J + 1
-// under the loads' latency, then the wait: one asm block (separate ones get
-// a wait state between them)
-template <int J>
-__device__ __forceinline__ void fent_pair(uint64_t ft, uint32_t o0, uint32_t o1, uint64_t& f0, uint64_t& f1,
-                                          uint32_t& buf, uint32_t a, uint32_t b) {
+__device__ __forceinline__ void fent_issue2n(uint64_t ft, uint32_t o0, uint32_t o1, uint64_t& f0, uint64_t& f1,
+                                             uint32_t& av) {  // no entries to park (the bulk's first pair)
     asm volatile(
         "s_load_dwordx2 %0, %3, %4\n\t"
-        "s_load_dwordx2 %1, %3, %5\n\t"
-        "v_writelane_b32 %2, %6, %8\n\t"
-        "v_writelane_b32 %2, %7, %9\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&s"(f0), "=&s"(f1), "+v"(buf)
-        : "s"(ft), "s"(o0), "s"(o1), "s"(a), "s"(b), "i"(J), "i"(J + 1));
+        "s_load_dwordx2 %1, %3, %5"
+        : "=&s"(f0), "=&s"(f1), "+s"(av)
+        : "s"(ft), "s"(o0), "s"(o1));
+}
+__device__ __forceinline__ void fent_wait2(uint64_t& f0, uint64_t& f1, uint64_t& W, uint32_t& av) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(f0), "+s"(f1), "+s"(W), "+s"(av));
+}
+template <int J>
+__device__ __forceinline__ void fent_issue1(uint64_t ft, uint32_t o, uint64_t& f, uint32_t& buf, uint32_t a,
+                                            uint32_t& av) {
+    asm volatile(
+        "s_load_dwordx2 %0, %3, %4\n\t"
+        "v_writelane_b32 %1, %5, %6"
+        : "=&s"(f), "+v"(buf), "+s"(av)
+        : "s"(ft), "s"(o), "s"(a), "i"(J));
+}
+__device__ __forceinline__ void fent_issue1n(uint64_t ft, uint32_t o, uint64_t& f, uint32_t& av) {
+    asm volatile("s_load_dwordx2 %0, %2, %3" : "=&s"(f), "+s"(av) : "s"(ft), "s"(o));
+}
+__device__ __forceinline__ void fent_wait1(uint64_t& f, uint64_t& W, uint32_t& av) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(f), "+s"(W), "+s"(av));
 }
 
 template <int NS>
@@ -1899,30 +1898,28 @@ __global__ __launch_bounds__(64) void single_decode_kernel(DecParams P) {
                 uint32_t g = min(by_bits, by_cap);
                 if (g == 0u) break;
                 uint32_t x0 = s0 << 3, x1 = s1 << 3;  // the states as byte offsets into ft
+                uint64_t fa0, fa1, fb0, fb1;  // entries of even / odd steps
+                fent_issue2n(ft, x0, x1, fa0, fa1, av);
                 for (; g; --g) {
-                    uint64_t p0 = 0, p1 = 0;  // the previous pair's entries
                     auto step = [&](auto J) {
                         constexpr int j = decltype(J)::value;
-                        uint64_t f0, f1;
-                        if (j > 0) {
-                            fent_pair<2 * j - 2>(ft, x0, x1, f0, f1, eb, (uint32_t)p0, (uint32_t)p1);
-                        } else {
-                            fent_load2(ft, x0, x1, f0, f1);
-                            fent_wait(f0, f1);
-                        }
-                        uint32_t op = av + (uint32_t)f0;
-                        x0 = fstep(W, op, (uint32_t)(f0 >> 32));
-                        op = (op & 0xFFFFu) + (uint32_t)f1;
-                        x1 = fstep(W, op, (uint32_t)(f1 >> 32));
+                        uint64_t& c0 = (j & 1) ? fb0 : fa0;
+                        uint64_t& c1 = (j & 1) ? fb1 : fa1;
+                        uint64_t& n0 = (j & 1) ? fa0 : fb0;
+                        uint64_t& n1 = (j & 1) ? fa1 : fb1;
+                        fent_wait2(c0, c1, W, av);
+                        uint32_t op = av + (uint32_t)c0;
+                        x0 = fstep(W, op, (uint32_t)(c0 >> 32));
+                        op = (op & 0xFFFFu) + (uint32_t)c1;
+                        x1 = fstep(W, op, (uint32_t)(c1 >> 32));
                         av = op & 0xFFFFu;
+                        fent_issue2<2 * j>(ft, x0, x1, n0, n1, eb, (uint32_t)c0, (uint32_t)c1, av);
                         refill();  // a pair takes <= 2L = 22 bits, a refill leaves >= 32
-                        p0 = f0;
-                        p1 = f1;
                     };
                     unroll<32>(step);
-                    park2<62>(eb, (uint32_t)p0, (uint32_t)p1);
                     put64();
                 }
+                fent_wait2(fa0, fa1, W, av);  // the loads issued after the last pair
                 s0 = x0 >> 3;
                 s1 = x1 >> 3;
             }
@@ -1966,27 +1963,24 @@ __global__ __launch_bounds__(64) void single_decode_kernel(DecParams P) {
                 uint32_t g = min(by_bits, by_cap);
                 if (g == 0u) break;
                 uint32_t x = s << 3;
+                uint64_t fa, fb;  // entries of even / odd steps
+                fent_issue1n(ft, x, fa, av);
                 for (; g; --g) {
-                    uint64_t p = 0, dummy = 0;
                     auto step = [&](auto J) {
                         constexpr int j = decltype(J)::value;
-                        uint64_t f;
-                        if (j > 0) {
-                            fent_one<j - 1>(ft, x, f, eb, (uint32_t)p);
-                        } else {
-                            fent_load1(ft, x, f);
-                            fent_wait(f, dummy);
-                        }
-                        const uint32_t op = av + (uint32_t)f;
-                        x = fstep(W, op, (uint32_t)(f >> 32));
+                        uint64_t& c = (j & 1) ? fb : fa;
+                        uint64_t& nx = (j & 1) ? fa : fb;
+                        fent_wait1(c, W, av);
+                        const uint32_t op = av + (uint32_t)c;
+                        x = fstep(W, op, (uint32_t)(c >> 32));
                         av = op & 0xFFFFu;
+                        fent_issue1<j>(ft, x, nx, eb, (uint32_t)c, av);
                         if (j & 1) refill();  // two symbols take <= 2L = 22 bits
-                        p = f;
                     };
                     unroll<64>(step);
-                    park<63>(eb, (uint32_t)p);
                     put64();
                 }
+                fent_wait1(fa, W, av);
                 s = x >> 3;
             }
             for (;;) {  // lib.rs:198-207 with the read check, then finish (208)
