@@ -144,3 +144,24 @@ def test_reference_kats_through_hip_normalize(torch_cuda):
         assert list(nh.norm)[: log2 + 1] == [size >> (1 + j) for j in range(log2 - 1)] + [-1, -1], log2
         assert all(v == 0 for v in list(nh.norm)[log2 + 1:])
         verify(h, nh, log2)
+
+
+@pytest.mark.parametrize("nstates", [2, 1])
+def test_host_calls_past_the_pinned_window(torch_cuda, nstates):
+    """Per-call entry points whose compressed and decoded bytes exceed the 4 MiB
+    pinned return window (fse_capi.cpp kPinOut): the head comes back through
+    pinned memory, the rest by a device-to-host copy; bytes equal the oracle's
+    and the stream decodes back exactly (near-uniform data, ~1 B per byte)."""
+    from entropy_coders_amd import compress, compress2, decompress, decompress2
+
+    src = O.generate(2, 0.0, 0x5EED0007, 0, (6 << 20) + 12345)
+    if nstates == 2:
+        comp, bits = compress2(src)
+        assert (comp, bits) == O.compress2(src)
+        assert len(comp) > (4 << 20)
+        assert decompress2(comp, cap=len(src) + 64) == src.tobytes()
+    else:
+        comp, bits = compress(src)
+        assert (comp, bits) == O.compress(src)
+        assert len(comp) > (4 << 20)
+        assert decompress(comp, cap=len(src) + 64) == src.tobytes()
