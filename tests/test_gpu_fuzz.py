@@ -281,3 +281,51 @@ def test_serial_deferred_symbols(torch_cuda, defer, nstates):
             f"t._check_serial(torch, {nstates}); print('child-ok')")
     r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "child-ok" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
+
+
+@pytest.mark.parametrize("nstates", [2, 1])
+@pytest.mark.parametrize("seed", range(4))
+def test_host_decode_damaged_streams(torch_cuda, nstates, seed):
+    """The host fse_decompress2 / fse_decompress (single_decode_kernel at table
+    logs <= 11, the serial kernels above) on damaged crate streams and at
+    random capacities: the decoded bytes, or the status, equal the oracle's
+    reference-mode result (lib.rs:187-248: None -> a status, a full Vec ->
+    DST_TOO_SMALL)."""
+    from entropy_coders_amd import FseError, compress, compress2, compress2_log, decompress, decompress2
+
+    rng = np.random.default_rng(0xDA3A6E + 17 * seed + nstates)
+    for case in range(24):
+        n = int(rng.integers(3, 9000))
+        s = O.generate(int(rng.integers(0, 3)), float(rng.uniform(0.05, 0.8)), int(rng.integers(1 << 30)), 0, n)
+        if len(set(s.tolist())) < 2:
+            continue
+        L = int(rng.choice([0, 0, 9, 11, 12]))
+        try:
+            if nstates == 2:
+                comp = (compress2_log(s, L) if L else compress2(s))[0]
+                dec, rdec = decompress2, O.decompress2
+            else:
+                comp = compress(s)[0]
+                dec, rdec = decompress, O.decompress
+        except FseError:  # e.g. a table log the histogram cannot take (the oracle agrees: test_random_host_calls)
+            continue
+        b = bytearray(comp)
+        what = int(rng.integers(0, 5))
+        if what == 1 and len(b) > 8:  # flip a payload bit
+            i = int(rng.integers(len(b) // 2, len(b)))
+            b[i] ^= 1 << int(rng.integers(0, 8))
+        elif what == 2 and len(b) > 4:  # truncate
+            b = b[: int(rng.integers(1, len(b)))]
+        elif what == 3:  # a different last byte (the marker)
+            b[-1] = int(rng.integers(0, 256))
+        elif what == 4 and len(b) > 2:  # damage the header
+            b[int(rng.integers(0, min(len(b), 6)))] ^= 1 << int(rng.integers(0, 8))
+        cap = int(rng.choice([n + 64, max(1, n // 2), n, 4 * n + 4096]))
+        try:
+            want = rdec(bytes(b), cap=cap)
+        except O.OracleError as e:
+            with pytest.raises(FseError) as g:
+                dec(bytes(b), cap=cap)
+            assert g.value.code == e.code, (seed, case, what, cap)
+            continue
+        assert dec(bytes(b), cap=cap) == want, (seed, case, what, cap)
