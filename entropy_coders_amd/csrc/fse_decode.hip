@@ -266,6 +266,18 @@ struct LdsChain {
             asm volatile("; pad %0 %1 %2 %3" ::"v"(d0), "v"(d1), "v"(d2), "v"(d3));
         }
 #endif
+#if FSEHIP_ABL & 256  // sensitivity probe (timing only): one more random table-like LDS read per pair
+        {
+            const uint32_t dx = *reinterpret_cast<const uint32_t*>(dtb + (((a1 ^ (a0 << 7)) * 0x9E3779B1u >> 19) & 0x1FFCu));
+            asm volatile("; sink %0" ::"v"(dx));
+        }
+#endif
+#if FSEHIP_ABL & 512  // sensitivity probe (timing only): one more payload-like LDS read per pair (the word below)
+        {
+            const uint32_t dx = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(pay) + (lo >> 3) - 4);
+            asm volatile("; sink %0" ::"v"(dx));
+        }
+#endif
         return __builtin_amdgcn_perm(e1, e0, 0x0c0c0501u);  // sym0 | sym1 << 8
     }
     __device__ __forceinline__ uint32_t s0() const { return a0 >> 2; }
