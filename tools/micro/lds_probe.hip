@@ -7,6 +7,9 @@
 //   gather_u16_16 x = tab16[x], 16-bank half-tables by lane bit 4
 //   hist_cur      ds_add_u32 in the encoder's histogram layout (16 copies, 16-bit halves)
 //   hist_lane     ds_add_u32, one private 8-bit-counter column per lane (bank = lane)
+//   bperm2        two ds_bpermute_b32 per step from 64-entry register tables
+//                 (the symbol transforms of a block with <= 64 symbols held in
+//                 two VGPRs instead of an LDS array: dNB and dFS)
 // Byte values for the histograms: geometric p = 1/2 (skewed) or uniform.
 // Build: hipcc -O3 --offload-arch=gfx950 lds_probe.hip -o lds_probe
 #include <hip/hip_runtime.h>
@@ -62,6 +65,16 @@ __global__ __launch_bounds__(256) void probe(const uint32_t* __restrict__ init, 
                 const uint32_t i = x[c] & 2047u;  // entry i: word (i / 2) -> row (i / 32), bank (i / 2) % 16
                 const uint32_t w = ((i >> 5) << 5) + half * 16u + ((i >> 1) & 15u);
                 x[c] = t16[2u * w + (i & 1u)] ^ (x[c] >> 11);
+            }
+    } else if (V == 6) {
+        const uint32_t r0 = init[lane], r1 = init[64 + lane];  // two 64-entry register tables
+        for (int s = 0; s < STEPS; ++s)
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const int a = (int)((x[c] & 63u) << 2);
+                const uint32_t u = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)r0);
+                const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)r1);
+                x[c] = u ^ (v >> 3);
             }
     } else if (V == 4 || V == 5) {
         uint32_t r = mix(threadIdx.x + blockIdx.x * 256u);
@@ -152,6 +165,7 @@ int main() {
         run<1>("gather_u16", d_init, d_lut, d_out, d_clk, w);
         run<2>("gather_b64", d_init, d_lut, d_out, d_clk, w);
         run<3>("gather_u16_16", d_init, d_lut, d_out, d_clk, w);
+        run<6>("bperm2", d_init, d_lut, d_out, d_clk, w);
         run<4>("hist_cur_geo", d_init, d_lut, d_out, d_clk, w);
         run<5>("hist_lane_geo", d_init, d_lut, d_out, d_clk, w);
         run<4>("hist_cur_uni", d_init, nullptr, d_out, d_clk, w);
