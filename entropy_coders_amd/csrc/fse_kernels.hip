@@ -39,15 +39,8 @@ __device__ __forceinline__ uint4 load_chunk(const uint8_t* blk, uint32_t n, uint
 // stateTable[deltaFindState]} (fse.rs:165-188): the block's table base is
 // folded into the transform, so one state step is add, shift, shift-add,
 // ds_read_u16 whichever table of the workgroup the lane uses.
-#ifndef FSEHIP_ENC_BPERM
-#define FSEHIP_ENC_BPERM 0  // A/B: symbol transforms of blocks with <= 64 symbols from two VGPRs (ds_bpermute)
-#endif
 struct EncTab {
     const uint2* tt;  // {deltaNbBits, LDS address of stateTable + 2 * deltaFindState}
-#if FSEHIP_ENC_BPERM
-    uint32_t rnb, rfs;  // lane s: tt[s].x, tt[s].y (symbols 0..63)
-    bool bp;            // table_len <= 64 and one block per wave: look up through the registers
-#endif
 };
 typedef __attribute__((address_space(3))) const uint16_t lds_cu16;
 __device__ __forceinline__ uint32_t st_at(uint32_t lds_addr) {
@@ -235,28 +228,11 @@ __device__ __forceinline__ void enc_chunk(const uint4& q, uint32_t c8, uint32_t 
     // all 16 symbol transforms depend only on the chunk: issue their LDS
     // reads up front so only the stateTable reads sit on the state chain
     uint2 t0[8], t1[8];
-#if FSEHIP_ENC_BPERM
-    if (T.bp) {  // symbols < 64: lane s of two registers, through the LDS crossbar (no bank access)
-        auto bp2 = [&](uint32_t sym) {
-            const int a = (int)(sym << 2);
-            return make_uint2((uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)T.rnb),
-                              (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)T.rfs));
-        };
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const uint32_t sh = 16u * (uint32_t)(j & 1);
-            t0[j] = bp2((w[j >> 1] >> sh) & 0x3Fu);
-            t1[j] = bp2((w[j >> 1] >> (sh + 8u)) & 0x3Fu);
-        }
-    } else
-#endif
-    {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const uint32_t sh = 16u * (uint32_t)(j & 1);
-            t0[j] = T.tt[(w[j >> 1] >> sh) & 0xFFu];
-            t1[j] = T.tt[(w[j >> 1] >> (sh + 8u)) & 0xFFu];
-        }
+    for (int j = 0; j < 8; ++j) {
+        const uint32_t sh = 16u * (uint32_t)(j & 1);
+        t0[j] = T.tt[(w[j >> 1] >> sh) & 0xFFu];
+        t1[j] = T.tt[(w[j >> 1] >> (sh + 8u)) & 0xFFu];
     }
     if (NS == 1) {
 #pragma unroll
@@ -483,7 +459,6 @@ struct EncSmem {
     } ph;
     int32_t info_status[BPW];
     uint32_t info_L[BPW];
-    uint32_t info_tl[BPW];  // table_len
     uint32_t info_hl[BPW];
     uint32_t info_hv[BPW];  // the header's last partial word (merged with the payload's first bits)
     int scratch[4];
@@ -594,7 +569,6 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
         if (lane == 0) {
             sm.info_status[b] = rc;
             sm.info_L[b] = L;
-            sm.info_tl[b] = tl;
             sm.info_hl[b] = (rc == FSE_OK) ? (uint32_t)sm.scratch[1] : 0u;
             if (rc != FSE_OK) {
                 P.status[gb] = rc;
@@ -616,11 +590,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     const uint32_t n = live ? (uint32_t)min((uint64_t)P.block_size, P.n_total - boff) : 0u;
     const uint8_t* blk = P.src + boff;
     const uint32_t L = sm.info_L[b];
-#if FSEHIP_ENC_BPERM
-    const EncTab tab{sm.tt[b], sm.tt[b][lane].x, sm.tt[b][lane].y, BPW == 1 && sm.info_tl[b] <= 64u};
-#else
     const EncTab tab{sm.tt[b]};
-#endif
     // main-loop steps: pairs (NS = 2) or symbols below the seed (NS = 1)
     const uint32_t Pm = live ? (NS == 2 ? ((n & 1u) ? (n - 3u) / 2u : n / 2u - 1u) : n - 1u) : 0u;
     constexpr uint32_t SPC = NS == 2 ? 8u : 16u;  // steps per 16-byte chunk
