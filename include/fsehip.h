@@ -55,7 +55,16 @@ int fse_compress2_log(const uint8_t* src, size_t n, uint32_t table_log, uint8_t*
  * -> Option<usize>` (lib.rs:215).  Appends the decoded bytes at
  * dst[*dst_len] and advances *dst_len.  None -> BAD_HEADER / NO_MARKER;
  * the state-read panic -> TOO_SHORT; the never-terminating single-symbol
- * case -> SINGLE_SYMBOL. */
+ * case -> SINGLE_SYMBOL; output beyond dst_cap -> DST_TOO_SMALL (the
+ * reference grows its Vec).
+ *
+ * The host entry points of this section are synchronous on the default
+ * stream and stage through per-thread buffers the library keeps: pinned host
+ * memory (the input, and up to 4 MiB of the result; larger results come back
+ * by a plain device-to-host copy) and device memory (input, output up to
+ * dst_cap - *dst_len, tables).  fsehip_release_workspace frees them.  A lone
+ * stream decodes as one serial chain (~1.4 ms per 64 KiB call on MI355X);
+ * many streams belong on fsehip_decompress_streams. */
 int fse_decompress2(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, size_t* dst_len);
 
 /* The 1-state format: replaces `pub fn fse_compress(src, dst) -> (NormHistogram, usize)`
