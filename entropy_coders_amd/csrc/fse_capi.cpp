@@ -35,7 +35,15 @@ uint64_t round_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 // synchronises the stream (the work of earlier holders has been enqueued on
 // it) before freeing the old one.  Different streams get different
 // workspaces.
-enum { SCRATCH_DT = 0, SCRATCH_DTINFO = 1, SCRATCH_BITS = 2, SCRATCH_STATES = 3, SCRATCH_BULK = 4, SCRATCH_KINDS = 5 };
+enum {
+    SCRATCH_DT = 0,
+    SCRATCH_DTINFO = 1,
+    SCRATCH_BITS = 2,
+    SCRATCH_STATES = 3,
+    SCRATCH_BULK = 4,
+    SCRATCH_HDR = 5,  // the lane-parallel header parse's output (optional)
+    SCRATCH_KINDS = 6
+};
 struct Workspace {
     int dev;
     void* stream;
@@ -506,12 +514,23 @@ static int decompress_impl(const fsehip_params* p, const uint8_t* d_in, uint64_t
 
 uint64_t fsehip_dtable_bytes(uint32_t max_table_log) { return 4ull << kern_lmax(max_table_log); }
 
-int fsehip_build_dtables(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes, const uint32_t* d_comp_len,
-                         uint32_t n_blocks, uint32_t* d_dtables, int32_t* d_dtinfo, fsehip_stream_t stream) {
+// The table build; `lease` (held by the caller) supplies the header-parse
+// scratch when the batch is large enough for the lane-parallel parse to pay
+// (a workgroup parses 64 headers), else the table kernel parses on its own.
+static int build_dtables_impl(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
+                              const uint32_t* d_comp_len, uint32_t n_blocks, uint32_t* d_dtables, int32_t* d_dtinfo,
+                              fsehip_stream_t stream, Lease* lease) {
     if (!p || !d_in || !d_comp_len || !d_dtables || !d_dtinfo || (slot_bytes & 255u)) return FSE_ERR_BAD_ARG;
     if (n_blocks == 0) return FSE_OK;
     if (!device_ok()) return FSE_ERR_NO_DEVICE;
     fsehip::DtParams D{};
+    if (lease && n_blocks >= 256u && kern_lmax(p->max_table_log) <= 12 && !env_u32("FSEHIP_DT_WAVE_PARSE", 0)) {
+        uint8_t* h = static_cast<uint8_t*>(lease->get(SCRATCH_HDR, fsehip::hdr_scratch_bytes(n_blocks), true));
+        if (h) {
+            D.hdr_norm = reinterpret_cast<uint32_t*>(h);
+            D.hdr_meta = reinterpret_cast<int2*>(h + 512ull * n_blocks);
+        }
+    }
     D.in = d_in;
     D.slot_bytes = slot_bytes;
     D.comp_len = d_comp_len;
@@ -523,6 +542,14 @@ int fsehip_build_dtables(const fsehip_params* p, const uint8_t* d_in, uint64_t s
     hipError_t e = fsehip::launch_dtables(D, kern_lmax(p->max_table_log), static_cast<hipStream_t>(stream));
     if (D.stamps) g_stamps_dt.report("dtables", n_blocks, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? FSE_OK : FSE_ERR_HIP;
+}
+
+int fsehip_build_dtables(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes, const uint32_t* d_comp_len,
+                         uint32_t n_blocks, uint32_t* d_dtables, int32_t* d_dtinfo, fsehip_stream_t stream) {
+    if (n_blocks < 256u) return build_dtables_impl(p, d_in, slot_bytes, d_comp_len, n_blocks, d_dtables, d_dtinfo, stream,
+                                                   nullptr);
+    Lease lease(stream);  // the header-parse scratch
+    return build_dtables_impl(p, d_in, slot_bytes, d_comp_len, n_blocks, d_dtables, d_dtinfo, stream, &lease);
 }
 
 int fsehip_decompress_blocks_dt(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
@@ -553,7 +580,7 @@ static int with_dtables_n(const fsehip_params* p, const uint8_t* d_in, uint64_t 
     uint32_t* dt = static_cast<uint32_t*>(lease.get(SCRATCH_DT, fsehip_dtable_bytes(p->max_table_log) * n_blocks));
     int32_t* info = static_cast<int32_t*>(lease.get(SCRATCH_DTINFO, 4ull * n_blocks));
     if (!dt || !info) return FSE_ERR_HIP;
-    int rc = fsehip_build_dtables(p, d_in, slot_bytes, d_comp_len, (uint32_t)n_blocks, dt, info, stream);
+    int rc = build_dtables_impl(p, d_in, slot_bytes, d_comp_len, (uint32_t)n_blocks, dt, info, stream, &lease);
     return rc != FSE_OK ? rc : run(dt, info, lease);
 }
 template <class Run>

@@ -821,6 +821,66 @@ __global__ __launch_bounds__(NT) void decode_pre_kernel(DecParams P) {
 }
 
 // ------------------------------------------------------------------------
+// NormHistogram::read (histogram.rs:436-505) for 16 blocks per wave, one lane
+// per block.  Parsed on the scalar unit inside dtable_blocks_kernel a header
+// costs ~2,200 scalar instructions, and at full occupancy the CU's one scalar
+// unit is shared by all its waves (the parse took 29.8K of the kernel's 68.4K
+// cycles per block, profiles/r04/probe1/stamps_T64.log).  Here the headers
+// are staged into LDS rows (the same 512 bytes the wave parse holds, coalesced
+// per block, 16 blocks' loads in flight at once) and each lane runs the same
+// parse (header_read_core) on its own row; the counts and the header length /
+// L / table_len go to the scratch that dtable_blocks_kernel then reads.
+// ------------------------------------------------------------------------
+constexpr uint32_t HP_BLOCKS = 16;  // headers per workgroup: 1,024 workgroups at C2 (8 measured no faster: the parse latency is the floor)
+template <int LMAX>
+__global__ __launch_bounds__(64) void hdr_parse_kernel(DtParams P) {
+    static_assert(LMAX <= 12, "headers of L <= 12 fit the 512 staged bytes");
+    constexpr uint32_t NB = HP_BLOCKS;
+    // block j's header words and counts, rotated by j words (row j, word i at
+    // (i + j) % 128): lanes at the same word index hit different banks
+    __shared__ uint32_t rows[NB][128];
+    __shared__ uint32_t nrm[NB][128];  // 256 x int16 per block
+    const uint32_t lane = threadIdx.x;
+    const uint64_t gb0 = (uint64_t)blockIdx.x * NB;
+    const uint64_t gl = gb0 + lane;
+    const bool mine = lane < NB && gl < P.n_blocks;
+    const uint32_t clen_l = mine ? P.comp_len[gl] : 0u;
+    // the words header_read_wave holds: min(clen, 512) bytes, within the slot
+    const uint32_t nw_l = (uint32_t)min((uint64_t)min(clen_l, HDR_MAX) + 3u, P.slot_bytes) >> 2;
+    for (uint32_t i = lane; i < NB * 128u; i += 64u) (&nrm[0][0])[i] = 0u;
+    // stage: block j's words across the lanes, every block's loads in flight at once
+    uint32_t a[NB], b[NB];
+#pragma unroll
+    for (uint32_t j = 0; j < NB; ++j) {
+        const uint32_t nw = (uint32_t)__builtin_amdgcn_readlane((int)nw_l, (int)j);  // 0 past the batch
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(P.in + (gb0 + j) * P.slot_bytes);
+        a[j] = lane < nw ? w[lane] : 0u;
+        b[j] = lane + 64u < nw ? w[lane + 64u] : 0u;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < NB; ++j) {
+        rows[j][(lane + j) & 127u] = a[j];
+        rows[j][(lane + 64u + j) & 127u] = b[j];
+    }
+    __syncthreads();
+    if (mine) {
+        uint32_t L = 0, tl = 0;
+        typedef __attribute__((address_space(3))) int16_t lds_i16;
+        const int hl = header_read_row((const lds_u32*)&rows[lane][0], lane, nw_l, clen_l, (uint32_t)LMAX,
+                                       (lds_i16*)&nrm[lane][0], &L, &tl);
+        P.hdr_meta[gl] = make_int2(hl, (int)(L | (tl << 8)));
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < NB; ++j) {  // counts out, unrotated: word k of block j
+        const uint64_t g = gb0 + j;
+        if (g >= P.n_blocks) break;
+        P.hdr_norm[g * 128u + lane] = nrm[j][(lane + j) & 127u];
+        P.hdr_norm[g * 128u + 64u + lane] = nrm[j][(lane + 64u + j) & 127u];
+    }
+}
+
+// ------------------------------------------------------------------------
 // Decode tables for a batch of blocks (C3's "pre-built dtables"; also the
 // first kernel of the two-kernel decode): NormHistogram::read on the scalar
 // unit + DecodeTable (fse.rs:280-338) by one wave per block, written to HBM
@@ -848,30 +908,46 @@ __global__ __launch_bounds__(64) void dtable_blocks_kernel(DtParams P) {
     FSE_STAMP(P, 0);
     const uint8_t* in = P.in + gb * P.slot_bytes;
     const uint32_t clen = P.comp_len[gb];
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(in);
-    // The header words are loaded before the length arrives when the slot
-    // holds HDR_MAX bytes (always, for encoder slots), so the two loads and
-    // the marker byte's load overlap instead of following one another;
-    // words past the block are zeroed once the length is known.
-    uint32_t r0, r1;
-    if (P.slot_bytes >= HDR_MAX) {
-        r0 = w[lane];
-        r1 = w[lane + 64u];
-    }
     const uint32_t last = (clen && clen <= P.slot_bytes) ? in[clen - 1u] : 0u;
-    const uint32_t nw = (uint32_t)min((uint64_t)min(clen, HDR_MAX) + 3u, P.slot_bytes) >> 2;
-    if (P.slot_bytes < HDR_MAX) {
-        r0 = lane < nw ? w[lane] : 0u;
-        r1 = lane + 64u < nw ? w[lane + 64u] : 0u;
-    }
-    r0 = lane < nw ? r0 : 0u;
-    r1 = lane + 64u < nw ? r1 : 0u;
-    for (uint32_t s = lane; s < 256u; s += WAVE) norm[s] = 0;
-    wave_sync();
     uint32_t L = 0, tl = 0;
-    FSE_STAMP(P, 1);
-    const int hl = header_read_wave(r0, r1, clen, (uint32_t)LMAX, norm, &L, &tl);
-    FSE_STAMP(P, 2);
+    int hl;
+    if (LMAX <= 12 && P.hdr_meta) {  // parsed by hdr_parse_kernel: counts from the scratch
+        const int2 m = P.hdr_meta[gb];
+        const uint32_t q0 = P.hdr_norm[gb * 128u + lane], q1 = P.hdr_norm[gb * 128u + 64u + lane];
+        norm[2u * lane] = (int32_t)(int16_t)(q0 & 0xFFFFu);
+        norm[2u * lane + 1u] = (int32_t)(int16_t)(q0 >> 16);
+        norm[128u + 2u * lane] = (int32_t)(int16_t)(q1 & 0xFFFFu);
+        norm[128u + 2u * lane + 1u] = (int32_t)(int16_t)(q1 >> 16);
+        hl = m.x;
+        L = (uint32_t)m.y & 0xFFu;
+        tl = (uint32_t)m.y >> 8;
+        wave_sync();
+        FSE_STAMP(P, 1);
+        FSE_STAMP(P, 2);
+    } else {
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(in);
+        // The header words are loaded before the length arrives when the slot
+        // holds HDR_MAX bytes (always, for encoder slots), so the two loads and
+        // the marker byte's load overlap instead of following one another;
+        // words past the block are zeroed once the length is known.
+        uint32_t r0, r1;
+        if (P.slot_bytes >= HDR_MAX) {
+            r0 = w[lane];
+            r1 = w[lane + 64u];
+        }
+        const uint32_t nw = (uint32_t)min((uint64_t)min(clen, HDR_MAX) + 3u, P.slot_bytes) >> 2;
+        if (P.slot_bytes < HDR_MAX) {
+            r0 = lane < nw ? w[lane] : 0u;
+            r1 = lane + 64u < nw ? w[lane + 64u] : 0u;
+        }
+        r0 = lane < nw ? r0 : 0u;
+        r1 = lane + 64u < nw ? r1 : 0u;
+        for (uint32_t s = lane; s < 256u; s += WAVE) norm[s] = 0;
+        wave_sync();
+        FSE_STAMP(P, 1);
+        hl = header_read_wave(r0, r1, clen, (uint32_t)LMAX, norm, &L, &tl);
+        FSE_STAMP(P, 2);
+    }
     int rc = hl < 0 ? hl : FSE_OK;
     if (rc == FSE_OK && ((uint32_t)hl >= clen || last == 0)) rc = FSE_ERR_NO_MARKER;  // lib.rs:222
     if (rc == FSE_OK && clen > (1u << 28)) rc = FSE_ERR_UNSUPPORTED;  // bit positions are 32-bit in the decoders
@@ -2162,7 +2238,16 @@ int occupancy_report_dec(char* buf, int cap) {
     return len;
 }
 
-hipError_t launch_dtables(const DtParams& P, uint32_t lmax, hipStream_t stream) {
+hipError_t launch_dtables(const DtParams& P0, uint32_t lmax, hipStream_t stream) {
+    DtParams P = P0;
+    if (lmax > 12) P.hdr_meta = nullptr;  // the staged rows hold headers up to L = 12
+    if (P.hdr_meta && P.hdr_norm) {
+        const dim3 gp((P.n_blocks + HP_BLOCKS - 1u) / HP_BLOCKS);
+        if (lmax <= 11) hipLaunchKernelGGL((hdr_parse_kernel<11>), gp, dim3(64), 0, stream, P);
+        else hipLaunchKernelGGL((hdr_parse_kernel<12>), gp, dim3(64), 0, stream, P);
+    } else {
+        P.hdr_meta = nullptr;
+    }
     const dim3 g(P.n_blocks), b(64);
     if (lmax <= 11) hipLaunchKernelGGL((dtable_blocks_kernel<11>), g, b, P.xlds, stream, P);
     else if (lmax <= 12) hipLaunchKernelGGL((dtable_blocks_kernel<12>), g, b, P.xlds, stream, P);

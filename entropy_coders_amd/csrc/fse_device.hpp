@@ -668,21 +668,18 @@ __device__ inline int header_read_lane(const uint32_t* src, uint32_t n, uint32_t
 // norm value (no exec-mask change), and the zero-run marks (456-464) and the
 // loop's end conditions leave the common path through one branch.
 // ---------------------------------------------------------------------------
-__device__ inline int header_read_wave(uint32_t r0, uint32_t r1, uint32_t n, uint32_t lmax, int32_t* norm,
-                                       uint32_t* L_out, uint32_t* tl_out) {
+// The parse itself, over a word source ld(i) (word i of the header, zero
+// past the block) and a sink put(sym, value) for the normalised counts:
+// header_read_wave runs it wave-uniform on the scalar unit, header_read_row
+// one header per lane (hdr_parse_kernel).
+template <class LD, class PUT>
+__device__ __forceinline__ int header_read_core(LD ld, PUT put, uint32_t n, uint32_t lmax, uint32_t* L_out,
+                                                uint32_t* tl_out) {
     if (n == 0) return FSE_ERR_EMPTY;
     // a header is at most ~420 bytes: bounding the bit count keeps it in
     // int32 for any block (n*8 overflows above 2^28 bytes) without changing
     // where the header can run out
     const int32_t total = (int32_t)(min(n, 1u << 20) * 8u);
-    // r0 / r1 hold header words lane / 64 + lane (zero past the block): a
-    // word is one v_readlane.  Headers of L <= 12 fit in 417 bytes, so the
-    // 512 bytes held always cover them (L > lmax returns before reading on).
-    auto ld = [&](uint32_t i) -> uint32_t {
-        const uint32_t a = __builtin_amdgcn_readlane(r0, i & 63u);
-        const uint32_t b = __builtin_amdgcn_readlane(r1, i & 63u);
-        return i < 64u ? a : (i < 128u ? b : 0u);
-    };
     // window: words bw, bw+1; next bit = 32*bw + off; left = bits after it
     uint32_t bw = 0, off = 0;
     int32_t left = total;
@@ -719,7 +716,7 @@ __device__ inline int header_read_wave(uint32_t r0, uint32_t r1, uint32_t n, uin
         left -= (int32_t)adv;
         const int32_t sv = (int32_t)val - 1;
         rem -= (uint32_t)__builtin_abs(sv);  // stays >= 1 (val <= rem)
-        norm[sym] = sv;
+        put(sym, sv);
         sym += 1u;
         lg = 31u - (uint32_t)__builtin_clz(rem);
         thr = 1u << lg;
@@ -754,6 +751,32 @@ __device__ inline int header_read_wave(uint32_t r0, uint32_t r1, uint32_t n, uin
     *L_out = L;
     *tl_out = sym;
     return (total - left + 7) >> 3;
+}
+
+__device__ inline int header_read_wave(uint32_t r0, uint32_t r1, uint32_t n, uint32_t lmax, int32_t* norm,
+                                       uint32_t* L_out, uint32_t* tl_out) {
+    // r0 / r1 hold header words lane / 64 + lane (zero past the block): a
+    // word is one v_readlane.  Headers of L <= 12 fit in 417 bytes, so the
+    // 512 bytes held always cover them (L > lmax returns before reading on).
+    auto ld = [&](uint32_t i) -> uint32_t {
+        const uint32_t a = __builtin_amdgcn_readlane(r0, i & 63u);
+        const uint32_t b = __builtin_amdgcn_readlane(r1, i & 63u);
+        return i < 64u ? a : (i < 128u ? b : 0u);
+    };
+    // every lane stores the same norm value (no exec-mask change)
+    return header_read_core(ld, [&](uint32_t sym, int32_t sv) { norm[sym] = sv; }, n, lmax, L_out, tl_out);
+}
+
+// One header per lane: words from this lane's 128-word LDS row (the first nw
+// staged, as header_read_wave holds 512 bytes; word i at (i + rot) % 128, so
+// lanes at the same word read different banks), the counts as int16 into its
+// 256-entry LDS norm row, rotated the same way (zeroed by the caller).
+__device__ inline int header_read_row(const lds_u32* row, uint32_t rot, uint32_t nw, uint32_t n, uint32_t lmax,
+                                      __attribute__((address_space(3))) int16_t* norm, uint32_t* L_out,
+                                      uint32_t* tl_out) {
+    auto ld = [&](uint32_t i) -> uint32_t { return i < nw ? row[(i + rot) & 127u] : 0u; };
+    return header_read_core(
+        ld, [&](uint32_t sym, int32_t sv) { norm[(sym + 2u * rot) & 255u] = (int16_t)sv; }, n, lmax, L_out, tl_out);
 }
 
 // ---------------------------------------------------------------------------

@@ -70,7 +70,14 @@ struct DtParams {
     int32_t* dtinfo;   // header bytes | L << 16, or < 0 = status
     uint32_t xlds;     // diagnostics: extra dynamic LDS bytes per workgroup (occupancy probe)
     uint64_t* stamps;  // diagnostics: per-workgroup phase stamps (FSEHIP_STAMPS), or nullptr
+    // Optional scratch (lmax <= 12): the headers are parsed first, one lane
+    // per block (hdr_parse_kernel), and the table kernel reads the result
+    // instead of parsing on the scalar unit.  hdr_meta[b] = {header bytes or
+    // status, L | table_len << 8}; hdr_norm[b] = 256 x int16 counts (128 words).
+    int2* hdr_meta;
+    uint32_t* hdr_norm;
 };
+constexpr uint64_t hdr_scratch_bytes(uint64_t n_blocks) { return n_blocks * (512u + 8u); }
 
 struct GenParams {
     uint8_t* out;

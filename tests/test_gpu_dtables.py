@@ -145,3 +145,58 @@ def test_dual_chain_segments(torch_cuda, ckpt):
     stat = st2.cpu().numpy()
     assert STATUS[int(stat[5])] == "BAD_SIDECAR"
     assert (np.delete(stat, 5) == 0).all()
+
+
+@pytest.mark.parametrize("n_blocks", [320, 40])
+def test_dtables_damaged_headers(torch_cuda, n_blocks):
+    """Header parse at batch sizes on both sides of the lane-parallel parse
+    (hdr_parse_kernel, batches of >= 256 blocks; smaller ones parse on the
+    scalar unit inside the table kernel): blocks with damaged header bytes get
+    the oracle's NormHistogram::read status, the others its table, entry for
+    entry."""
+    torch = torch_cuda
+    from entropy_coders_amd import BlockCodec
+    from entropy_coders_amd._lib import STATUS
+
+    rng = np.random.default_rng(0xD7AB + n_blocks)
+    codec = BlockCodec(block_size=4096, ckpt_interval=64)
+    host = np.concatenate([O.generate(int(rng.integers(0, 3)), float(rng.uniform(0.05, 0.8)), int(rng.integers(1 << 30)),
+                                      b, 4096) for b in range(n_blocks)])
+    cb = codec.compress(torch.from_numpy(host).cuda())
+    torch.cuda.synchronize()
+    assert int(cb["status"].abs().max()) == 0
+    slots = cb["out"].cpu().numpy().copy()
+    lens = cb["comp_len"].cpu().numpy()
+    sb = codec.slot_bytes
+    for b in range(n_blocks):
+        if rng.random() < 0.5:
+            for _ in range(int(rng.integers(1, 4))):  # header bytes only: the marker stays
+                i = int(rng.integers(0, min(int(lens[b]) - 1, 40)))
+                slots[b * sb + i] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    cb["out"] = torch.from_numpy(slots).cuda()
+    tabs = codec.build_dtables(cb)
+    torch.cuda.synchronize()
+    info = tabs["info"].cpu().numpy()
+    per = int(codec.lib.fsehip_dtable_bytes(codec.max_table_log)) // 4
+    dt = tabs["dt"].cpu().numpy().view(np.uint32)
+    bad = 0
+    for b in range(n_blocks):
+        blk = slots[b * sb: b * sb + int(lens[b])].tobytes()
+        try:
+            L, ns, sym, nb, used = O.dtable(blk)
+        except O.OracleError as e:
+            assert info[b] == e.rc, (b, info[b], e.code)
+            bad += 1
+            continue
+        if L > codec.max_table_log:  # a valid header beyond this codec's tables (max_table_log 11)
+            assert STATUS[int(info[b])] == "UNSUPPORTED", (b, info[b])
+            bad += 1
+            continue
+        if used >= len(blk):  # the header ran into the marker byte: NO_MARKER (lib.rs:222)
+            assert info[b] < 0, b
+            continue
+        assert info[b] >= 0 and info[b] >> 16 == L and info[b] & 0xFFFF == used, (b, info[b])
+        e = dt[b * per: b * per + (1 << L)]
+        assert np.array_equal(e & 0xFF, nb) and np.array_equal((e >> 8) & 0xFF, sym), b
+        assert np.array_equal(e >> 18, ns), b
+    # (damaged headers often still parse: the oracle then gives the same other table)
