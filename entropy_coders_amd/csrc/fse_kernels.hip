@@ -39,6 +39,9 @@ __device__ __forceinline__ uint4 load_chunk(const uint8_t* blk, uint32_t n, uint
 // stateTable[deltaFindState]} (fse.rs:165-188): the block's table base is
 // folded into the transform, so one state step is add, shift, shift-add,
 // ds_read_u16 whichever table of the workgroup the lane uses.
+#ifndef FSEHIP_ENC_ABL
+#define FSEHIP_ENC_ABL 0  // encoder timing probes (variant builds only)
+#endif
 struct EncTab {
     const uint2* tt;  // {deltaNbBits, LDS address of stateTable + 2 * deltaFindState}
 };
@@ -121,7 +124,11 @@ struct Emit {
             store_words(skip_head ? w0 + 1u : w0, base + 8u);
         } else if (base + 8u <= wlim) {
             const uint4* r = reinterpret_cast<const uint4*>(ring + (base & 15u));
+#if FSEHIP_ENC_ABL & 1  // probe (timing only, wrong output): the same stores into the slot's first 2 KiB (L2-resident lines)
+            uint4* o = reinterpret_cast<uint4*>(gw + (base & 511u));
+#else
             uint4* o = reinterpret_cast<uint4*>(gw + base);
+#endif
             const uint4 a = r[0], b = r[1];
             o[0] = a;
             o[1] = b;
