@@ -284,7 +284,7 @@ def test_serial_deferred_symbols(torch_cuda, defer, nstates):
 
 
 @pytest.mark.parametrize("nstates", [2, 1])
-@pytest.mark.parametrize("seed", range(4))
+@pytest.mark.parametrize("seed", range(int(os.environ.get("FSEHIP_FUZZ_DAMAGE_SEEDS", 4))))
 def test_host_decode_damaged_streams(torch_cuda, nstates, seed):
     """The host fse_decompress2 / fse_decompress (single_decode_kernel at table
     logs <= 11, the serial kernels above) on damaged crate streams and at
