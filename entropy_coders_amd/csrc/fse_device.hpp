@@ -553,110 +553,11 @@ __device__ inline int wave_header_write(const int32_t* norm, uint32_t L, uint32_
 }
 
 // ---------------------------------------------------------------------------
-// NormHistogram::read (histogram.rs:436-505) + BitStreamReader semantics
-// (stream_reader.rs:16-135), one lane, reading global memory.  Returns the
-// consumed byte count (finish_byte) or < 0.
-// ---------------------------------------------------------------------------
-struct FwdReader {
-    const uint32_t* w;  // slice as little-endian words
-    uint32_t total;     // bits (8 * slice length, stream_reader.rs:16)
-    uint32_t pos;
-    uint32_t availw;    // words readable at w (bits past them read as 0)
-    uint32_t bufw;      // buf = words bufw, bufw+1
-    uint64_t buf;
-    __device__ __forceinline__ uint32_t load(uint32_t i) const { return i < availw ? w[i] : 0u; }
-    __device__ __forceinline__ void init(const uint32_t* words, uint32_t n_bytes, uint32_t avail_bytes) {
-        w = words;
-        total = n_bytes * 8u;
-        pos = 0;
-        availw = (min(avail_bytes, n_bytes) + 3u) >> 2;
-        bufw = 0;
-        buf = (uint64_t)load(0) | ((uint64_t)load(1) << 32);
-    }
-    __device__ __forceinline__ bool peek(uint32_t nb, uint32_t* v) {
-        if (pos + nb > total) return false;
-        while (pos >= (bufw + 1u) * 32u) {
-            bufw++;
-            buf = (buf >> 32) | ((uint64_t)load(bufw + 1u) << 32);
-        }
-        *v = (uint32_t)(buf >> (pos - bufw * 32u)) & ((1u << nb) - 1u);
-        return true;
-    }
-    __device__ __forceinline__ bool advance(uint32_t nb) {
-        if (pos + nb > total) return false;
-        pos += nb;
-        return true;
-    }
-};
-
-__device__ inline int header_read_lane(const uint32_t* src, uint32_t n, uint32_t avail, int32_t* norm,
-                                       uint32_t* L_out, uint32_t* tl_out) {
-    if (n == 0) return FSE_ERR_EMPTY;
-    FwdReader r;
-    r.init(src, n, avail);
-    uint32_t v;
-    if (!r.peek(4, &v)) return FSE_ERR_BAD_HEADER;
-    r.advance(4);
-    const uint32_t L = v + LOG_MIN;
-    if (L > LOG_MAX_REF) return FSE_ERR_BAD_HEADER;
-    for (uint32_t s = 0; s < 256; ++s) norm[s] = 0;
-    uint32_t sym = 0;
-    uint32_t thr = 1u << L;
-    uint32_t rem = thr + 1u;
-    uint32_t nb = L + 1u;
-    bool prev0 = false;
-    while (rem > 1 && sym < 256) {
-        if (prev0) {
-            for (;;) {
-                uint32_t pk;
-                if (!r.peek(16, &pk)) pk = 0;
-                if (pk != 0xFFFFu) break;
-                if (!r.advance(16)) return FSE_ERR_BAD_HEADER;
-                sym += 24;
-            }
-            for (;;) {
-                uint32_t pk;
-                if (!r.peek(2, &pk)) pk = 0;
-                if (pk != 3u) break;
-                if (!r.advance(2)) return FSE_ERR_BAD_HEADER;
-                sym += 3;
-            }
-            if (!r.peek(2, &v)) return FSE_ERR_BAD_HEADER;
-            r.advance(2);
-            sym += v;
-        }
-        if (sym >= 256) break;
-        const uint32_t mx = (2u * thr - 1u) - rem;
-        uint32_t raw;
-        if (!r.peek(nb, &raw) && !r.peek(nb - 1u, &raw)) return FSE_ERR_BAD_HEADER;
-        uint32_t val;
-        if ((raw & (thr - 1u)) < mx) {
-            if (!r.advance(nb - 1u)) return FSE_ERR_BAD_HEADER;
-            val = raw & (thr - 1u);
-        } else {
-            if (!r.advance(nb)) return FSE_ERR_BAD_HEADER;
-            val = raw & (2u * thr - 1u);
-            if (val >= thr) val -= mx;
-        }
-        int32_t sv = (int32_t)val - 1;
-        rem -= (uint32_t)(sv < 0 ? -sv : sv);
-        norm[sym] = sv;
-        sym += 1;
-        prev0 = (sv == 0);
-        while (rem < thr) { nb -= 1; thr >>= 1; }
-    }
-    if (rem != 1) return FSE_ERR_BAD_HEADER;
-    *L_out = L;
-    *tl_out = sym;
-    return (int)((r.pos + 7u) >> 3);
-}
-
-// ---------------------------------------------------------------------------
 // NormHistogram::read (histogram.rs:436-505) as wave-uniform code: every lane
 // of the calling wave holds the same values, so the serial parse runs on the
 // scalar unit (s_lshr_b64 window, s_flbit for the threshold) instead of one
-// VALU lane.  norm[] must be zeroed by the caller.  Same results and statuses
-// as header_read_lane.
+// VALU lane.  norm[] must be zeroed by the caller.  Results and statuses are
+// the reference's (stream_reader.rs:16-135 read / peek / advance semantics).
 //
 // The scalar unit is shared by the CU's waves, and the decode-table kernel is
 // bound by its issue rate (the parse is ~90% of that kernel's scalar
