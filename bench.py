@@ -301,7 +301,8 @@ def host_call_latency(reps: int = 20) -> dict:
     src = O.generate(0, 0.155, 0x5EED0002, 0, 65536)
     comp2, _ = compress2(src)
     comp1, _ = compress(src)
-    assert decompress2(comp2) == src.tobytes() and decompress(comp1) == src.tobytes()
+    if decompress2(comp2) != src.tobytes() or decompress(comp1) != src.tobytes():
+        raise RuntimeError("host-call round trip differs from the source")
 
     def med_us(fn):
         fn()
@@ -320,7 +321,8 @@ def host_call_latency(reps: int = 20) -> dict:
             "fse_compress_us": med_us(lambda: compress(src)),
             "fse_decompress_us": med_us(lambda: decompress(comp1, cap)),
             "oracle_compress2_us": med_us(lambda: O.compress2(src)),
-            "oracle_decompress2_us": med_us(lambda: O.decompress2(comp2, cap))}
+            "oracle_decompress2_us": med_us(lambda: O.decompress2(comp2, cap)),
+            "verified": True}
 
 
 FSE_ERR_ENCODER_INIT = -17  # include/fse_status.h
@@ -805,7 +807,14 @@ def main():
         if world == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(src.cpu().numpy(), args.block, args.cpu_seconds)
         if world == 1 and not args.no_host_calls:
-            line["host_call_latency"] = host_call_latency()
+            # after the verified step: a failure here is recorded in the line
+            # (and fails the run's verification) but never loses the line
+            try:
+                line["host_call_latency"] = host_call_latency()
+            except Exception as e:
+                line["host_call_latency"] = {"error": f"{type(e).__name__}: {e}"[:300], "verified": False}
+                ok = False
+                line["verified_roundtrip"] = False
         print(json.dumps(line), flush=True)
     if world > 1:
         # every rank stays until rank 0 has printed the line (a rank exiting

@@ -455,8 +455,11 @@ int fsehip_compress_blocks(const fsehip_params* p, const uint8_t* d_src, uint64_
 // 2^24 blocks or more (grid x threads >= 2^32) take the single-kernel decode.
 static void defer_symbols(Lease& lease, fsehip::DecParams& P, uint32_t lmax) {
     if (lmax > 11 || P.block_size < 2u || P.n_blocks >= (1u << 24) || !env_u32("FSEHIP_SERIAL_DEFER", 1)) return;
-    P.states = static_cast<uint32_t*>(lease.get(SCRATCH_STATES, 2ull * P.n_blocks * P.block_size, true));
+    // the small buffer first: when it cannot be had, the multi-GiB state
+    // buffer is never allocated (and never held by a decode that cannot use it)
     P.bulk = static_cast<uint32_t*>(lease.get(SCRATCH_BULK, 8ull * P.n_blocks, true));
+    P.states = P.bulk ? static_cast<uint32_t*>(lease.get(SCRATCH_STATES, 2ull * P.n_blocks * P.block_size, true))
+                      : nullptr;
     if (!P.states || !P.bulk) P.states = P.bulk = nullptr;
     if (env_u32("FSEHIP_SERIAL_DW", 1) == 2) P.pass = 7u;  // diagnostics: two decode waves (launch_decode)
 }

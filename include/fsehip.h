@@ -317,7 +317,11 @@ int fsehip_compress_blocks(const fsehip_params* p, const uint8_t* d_src, uint64_
  *                  (n_blocks x block_size) + 8 bytes per block -- 2 GiB for a
  *                  1 GiB batch.  A size that failed to allocate is remembered
  *                  (later calls of that size or more take the single-kernel
- *                  decode without retrying) until the next release.
+ *                  decode without retrying) until the next release;
+ *   header parse   520 bytes per block (the headers parsed one per lane
+ *                  before the table build: batches of >= 256 blocks at
+ *                  max_table_log <= 12, fsehip_build_dtables included;
+ *                  without it the tables kernel parses on its own).
  * Growing a buffer synchronises the stream before freeing the old one. */
 int fsehip_decompress_blocks(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
                              const uint32_t* d_comp_len, const uint64_t* d_sidecar, uint8_t* d_out,
@@ -328,7 +332,14 @@ int fsehip_decompress_blocks(const fsehip_params* p, const uint8_t* d_in, uint64
  * d_dtables holds fsehip_dtable_bytes(max_table_log) bytes per block (entry
  * u32 = nbBits | symbol << 8 | newState << 18 for max_table_log <= 14, and
  * newState << 17 at 15), d_dtinfo one int32 per
- * block (header bytes | tableLog << 16, or a negative status). */
+ * block (header bytes | tableLog << 16, or a negative status).
+ * The tables go to the caller's buffers, but a batch of >= 256 blocks at
+ * max_table_log <= 12 first parses its headers into the stream's workspace
+ * (520 bytes per block, the header-parse entry of the workspace note at
+ * fsehip_decompress_blocks): the call then holds that workspace's lock, so
+ * it is serialised with the library's other calls on the same stream, and
+ * growing the scratch synchronises the stream (the host blocks until the
+ * stream's earlier work is done).  fsehip_release_workspace frees it. */
 uint64_t fsehip_dtable_bytes(uint32_t max_table_log);
 int fsehip_build_dtables(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
                          const uint32_t* d_comp_len, uint32_t n_blocks, uint32_t* d_dtables, int32_t* d_dtinfo,
