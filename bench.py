@@ -295,7 +295,7 @@ def host_call_latency(reps: int = 20) -> dict:
     drop-ins: one 64 KiB C2 block per call, host buffers, PCIe copies and the
     kernels inside the call), median of `reps`, beside the oracle (the C
     restatement of the crate, -O3) on one host core doing the same call."""
-    from entropy_coders_amd import compress, compress2, decompress, decompress2
+    from entropy_coders_amd import compress, compress2, decompress, decompress2, decompress2_many
     from oracle import oracle as O
 
     src = O.generate(0, 0.155, 0x5EED0002, 0, 65536)
@@ -314,8 +314,20 @@ def host_call_latency(reps: int = 20) -> dict:
         return round(float(np.median(ts)) * 1e6, 1)
 
     cap = 1 << 17
+    # the batching drop-in: 1,000 crate streams (the oracle's bytes) in one call
+    many = [O.compress2(O.generate(0, 0.155, 0x5EED0002, i, 65536))[0] for i in range(1000)]
+    if decompress2_many(many[:8], 65536) != [O.generate(0, 0.155, 0x5EED0002, i, 65536).tobytes()
+                                             for i in range(8)]:
+        raise RuntimeError("fse_decompress2_many differs from the source")
+    t_many = med_us(lambda: decompress2_many(many, 65536))
+    t_one = med_us(lambda: [O.decompress2(c, cap) for c in many[:32]]) / 32
     return {"workload": "one 64 KiB C2 block per call (host buffers in and out), median of "
                         f"{reps} calls; oracle = the C restatement on one host core",
+            "fse_decompress2_many_1000": {"workload": "1,000 crate-format 64 KiB C2 streams in one "
+                                                      "fse_decompress2_many call (host buffers, PCIe included)",
+                                          "ms": round(t_many / 1e3, 3), "us_per_stream": round(t_many / 1000, 1),
+                                          "oracle_one_core_ms": round(t_one * 1000 / 1e3, 3),
+                                          "vs_one_core": round(t_one * 1000 / t_many, 2)},
             "fse_compress2_us": med_us(lambda: compress2(src)),
             "fse_decompress2_us": med_us(lambda: decompress2(comp2, cap)),
             "fse_compress_us": med_us(lambda: compress(src)),

@@ -29,7 +29,7 @@ EXPORTS = (
     "fsehip_generate", "fsehip_device_count", "fsehip_version",
     "fsehip_pack_blocks", "fsehip_unpack_blocks",
     "fsehip_dtable_bytes", "fsehip_build_dtables", "fsehip_decompress_blocks_dt",
-    "fse_compress", "fse_decompress", "fsehip_sidecar_per_block_ns",
+    "fse_compress", "fse_decompress", "fsehip_sidecar_per_block_ns", "fse_decompress2_many", "fse_decompress_many",
     "fsehip_copy_blocks", "fsehip_release_workspace",
     "histogram_new", "histogram_normalize", "histogram_normalize_optimal", "norm_histogram_new",
     "norm_histogram_write", "norm_histogram_read", "encode_table_new", "decode_table_new", "fse_compress_nh",
@@ -131,6 +131,8 @@ def load() -> C.CDLL:
     lib.fse_decompress2.argtypes = [P, sz, P, sz, C.POINTER(sz)]
     lib.fse_compress.argtypes = [P, sz, P, sz, C.POINTER(sz), C.POINTER(u64)]
     lib.fse_decompress.argtypes = [P, sz, P, sz, C.POINTER(sz)]
+    lib.fse_decompress2_many.argtypes = [P, P, sz, P, sz, P, P]
+    lib.fse_decompress_many.argtypes = [P, P, sz, P, sz, P, P]
     lib.histogram_count.argtypes = [P, sz, P, C.POINTER(u32)]
     lib.fsehip_slot_bytes.argtypes = [u32, u32]
     lib.fsehip_slot_bytes.restype = u64

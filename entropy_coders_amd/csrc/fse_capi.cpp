@@ -13,6 +13,7 @@
 #include <atomic>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/fsehip.h"
@@ -541,6 +542,7 @@ static int build_dtables_impl(const fsehip_params* p, const uint8_t* d_in, uint6
     D.dt = d_dtables;
     D.dtinfo = d_dtinfo;
     D.xlds = env_u32("FSEHIP_DT_XLDS", 0);  // diagnostics: occupancy probe
+    D.one_wave = env_u32("FSEHIP_DT_ONE_WAVE", 0);  // diagnostics: A/B of the table kernels
     D.stamps = g_stamps_dt.get(n_blocks);
     hipError_t e = fsehip::launch_dtables(D, kern_lmax(p->max_table_log), static_cast<hipStream_t>(stream));
     if (D.stamps) g_stamps_dt.report("dtables", n_blocks, static_cast<hipStream_t>(stream));
@@ -842,6 +844,144 @@ int fse_compress(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, siz
 
 int fse_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, size_t* dst_len) {
     return decompress_one(src, n, dst, dst_cap, dst_len, 1);
+}
+
+// Many host streams in one call: the batching pattern for a caller holding
+// many crate streams (lib.rs:187-248 per stream).  One pinned staging copy
+// in (lengths + streams at a common stride), the header parse + decode
+// tables + serial decoders of fsehip_decompress_streams on the default
+// stream (one chain per stream, thousands at once), one copy back of the
+// per-stream record (length, status) and output.  One or two streams take
+// the single-stream call instead (its chain is ~2x faster than one serial
+// ring chain, and the batch kernels' fixed cost buys nothing).
+// fn(i) for i in [0, n) on up to 16 host threads (contiguous ranges), one
+// thread per ~2 MB of copying: the staging memcpys of a large batch are the
+// call's host-side cost (one core copies ~5-10 GB/s).
+extern "C++" {
+template <class Fn>
+static void for_streams(size_t n, uint64_t bytes, Fn fn) {
+    const size_t T = (size_t)std::min<uint64_t>({16, (bytes >> 21) + 1, n});
+    if (T <= 1) {
+        for (size_t i = 0; i < n; ++i) fn(i);
+        return;
+    }
+    std::vector<std::thread> th;
+    th.reserve(T - 1);
+    auto range = [&](size_t t) {
+        for (size_t i = n * t / T; i < n * (t + 1) / T; ++i) fn(i);
+    };
+    for (size_t t = 1; t < T; ++t) th.emplace_back(range, t);
+    range(0);
+    for (auto& x : th) x.join();
+}
+}  // extern "C++"
+
+static int decompress_many(const uint8_t* const* srcs, const size_t* src_lens, size_t n_streams, uint8_t* dst,
+                           size_t dst_stride, size_t* dst_lens, int32_t* statuses, uint32_t nstates) {
+    if (n_streams == 0) return FSE_OK;
+    if (!srcs || !src_lens || !dst || !dst_lens || !statuses || dst_stride == 0) return FSE_ERR_BAD_ARG;
+    if (n_streams > (1u << 24) || dst_stride > 0x7FFFFFFFull) return FSE_ERR_UNSUPPORTED;
+    if (!device_ok()) return FSE_ERR_NO_DEVICE;
+    if (n_streams <= 2) {
+        for (size_t i = 0; i < n_streams; ++i) {
+            size_t len = 0;
+            statuses[i] = decompress_one(srcs[i], src_lens[i], dst + i * dst_stride, dst_stride, &len, nstates);
+            if (statuses[i] == FSE_ERR_HIP || statuses[i] == FSE_ERR_NO_DEVICE) return statuses[i];
+            dst_lens[i] = statuses[i] == FSE_OK ? len : 0;
+        }
+        return FSE_OK;
+    }
+    // per-stream statuses the reference's own checks give before any decode
+    size_t maxn = 1;
+    uint32_t lmax = 11;
+    for (size_t i = 0; i < n_streams; ++i) {
+        const size_t n = src_lens[i];
+        if (n == 0 || n > kMaxBlock || !srcs[i]) continue;
+        maxn = std::max(maxn, n);
+        lmax = std::max<uint32_t>(lmax, (uint32_t)(srcs[i][0] & 15u) + LOG_MIN_HOST);  // histogram.rs:438
+    }
+    const uint32_t mtl = lmax <= 11u ? 11u : lmax <= 12u ? 12u : 15u;
+    const uint64_t in_stride = round_up(maxn + 32, 256);
+    const uint64_t out_stride = round_up(dst_stride, 16);
+    const uint64_t head = round_up(4ull * n_streams, 256);  // the lengths ahead of the streams
+    const uint64_t in_bytes = head + in_stride * n_streams;
+    const uint64_t rec = round_up(8ull * n_streams, 256);  // (length, status) per stream ahead of the output
+    const uint64_t out_bytes = rec + out_stride * n_streams;
+    uint8_t* d_in = g_stage.get(4, in_bytes);
+    uint8_t* d_out = g_stage.get(5, out_bytes);
+    uint8_t* h_in = g_pin.get(0, in_bytes);
+    uint8_t* h_out = g_pin.get(1, out_bytes);
+    if (!d_in || !d_out || !h_in || !h_out) return FSE_ERR_HIP;
+    uint32_t* lens = reinterpret_cast<uint32_t*>(h_in);
+    uint64_t in_total = 0;
+    for (size_t i = 0; i < n_streams; ++i) in_total += src_lens[i] <= kMaxBlock ? src_lens[i] : 0;
+    for_streams(n_streams, in_total, [&](size_t i) {
+        const size_t n = src_lens[i];
+        const bool ok = n != 0 && n <= kMaxBlock && srcs[i];
+        uint8_t* s = h_in + head + i * in_stride;
+        lens[i] = ok ? (uint32_t)n : 0u;
+        if (ok) memcpy(s, srcs[i], n);
+        const size_t z = ok ? n : 0;
+        memset(s + z, 0, std::min<uint64_t>(in_stride, round_up(z, 32) + 32) - z);
+    });
+    auto fail = [](int rc) {  // nothing may still read or write the pinned buffers
+        (void)hipStreamSynchronize(nullptr);
+        return rc;
+    };
+    if (hipMemcpyAsync(d_in, h_in, in_bytes, hipMemcpyHostToDevice, nullptr) != hipSuccess) return fail(FSE_ERR_HIP);
+    const uint32_t* d_len = reinterpret_cast<const uint32_t*>(d_in);
+    uint32_t* d_olen = reinterpret_cast<uint32_t*>(d_out);
+    int32_t* d_stat = reinterpret_cast<int32_t*>(d_out + 4ull * n_streams);
+    const fsehip_params p{(uint32_t)out_stride, 0, 0, mtl, nstates};
+    int rc = with_dtables_n(&p, d_in + head, in_stride, d_len, n_streams, nullptr,
+                            [&](const uint32_t* dt, const int32_t* info, Lease& lease) {
+                                fsehip::DecParams P{};
+                                P.nstates = nstates;
+                                P.in = d_in + head;
+                                P.slot_bytes = in_stride;
+                                P.comp_len = d_len;
+                                P.out = d_out + rec;
+                                P.n_total = 0;  // reference mode: each stream ends where the crate stops
+                                P.block_size = (uint32_t)out_stride;
+                                P.n_blocks = (uint32_t)n_streams;
+                                P.out_cap = (uint32_t)dst_stride;
+                                P.status = d_stat;
+                                P.out_len = d_olen;
+                                P.dt = dt;
+                                P.dtinfo = info;
+                                defer_symbols(lease, P, kern_lmax(mtl));
+                                return fsehip::launch_decode(P, kern_lmax(mtl), nullptr) == hipSuccess
+                                           ? (int)FSE_OK
+                                           : (int)FSE_ERR_HIP;
+                            });
+    if (rc) return fail(rc);
+    if (hipMemcpyAsync(h_out, d_out, out_bytes, hipMemcpyDeviceToHost, nullptr) != hipSuccess) return fail(FSE_ERR_HIP);
+    if (hipStreamSynchronize(nullptr) != hipSuccess) return FSE_ERR_HIP;
+    const uint32_t* olen = reinterpret_cast<const uint32_t*>(h_out);
+    const int32_t* ost = reinterpret_cast<const int32_t*>(h_out + 4ull * n_streams);
+    uint64_t out_total = 0;
+    for (size_t i = 0; i < n_streams; ++i) out_total += ost[i] == FSE_OK ? olen[i] : 0;
+    for_streams(n_streams, out_total, [&](size_t i) {
+        const size_t n = src_lens[i];
+        int32_t st = ost[i];
+        if (n == 0) st = FSE_ERR_EMPTY;  // BitStreamReader::new asserts (stream_reader.rs:17)
+        else if (!srcs[i]) st = FSE_ERR_BAD_ARG;
+        else if (n > kMaxBlock) st = FSE_ERR_UNSUPPORTED;
+        statuses[i] = st;
+        dst_lens[i] = st == FSE_OK ? olen[i] : 0;
+        if (st == FSE_OK) memcpy(dst + i * dst_stride, h_out + rec + i * out_stride, olen[i]);
+    });
+    return FSE_OK;
+}
+
+int fse_decompress2_many(const uint8_t* const* srcs, const size_t* src_lens, size_t n_streams, uint8_t* dst,
+                         size_t dst_stride, size_t* dst_lens, int32_t* statuses) {
+    return decompress_many(srcs, src_lens, n_streams, dst, dst_stride, dst_lens, statuses, 2);
+}
+
+int fse_decompress_many(const uint8_t* const* srcs, const size_t* src_lens, size_t n_streams, uint8_t* dst,
+                        size_t dst_stride, size_t* dst_lens, int32_t* statuses) {
+    return decompress_many(srcs, src_lens, n_streams, dst, dst_stride, dst_lens, statuses, 1);
 }
 
 int histogram_count(const uint8_t* src, size_t n, uint32_t counts[256], uint32_t* table_len) {

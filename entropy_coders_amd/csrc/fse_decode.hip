@@ -970,6 +970,192 @@ __global__ __launch_bounds__(64) void dtable_blocks_kernel(DtParams P) {
 }
 
 // ------------------------------------------------------------------------
+// The same decode tables from hdr_parse_kernel's counts, one 256-thread
+// workgroup per block at L <= 11 (fse.rs:280-338 with the spread of
+// fse.rs:110-162): the table kernel above runs every step on one wave
+// (~45K cycles per table at full occupancy, latency-bound); here each step
+// is spread over 4 waves, one symbol or 8 positions per thread, with the
+// wave scans joined through LDS:
+//   1. per symbol (thread = symbol): the -1 / positive counts, block-wide
+//      exclusive sums -> start marks of each symbol's occurrences, the -1
+//      symbols from the top of the table;
+//   2. forward max-fill of the marks: owner of occurrence j;
+//   3. the spread walk, 8 multipliers per thread: position (m * step) & mask
+//      is kept iff <= the high threshold, the j-th kept gets occurrence j;
+//   4. ranks: per 64-position chunk, each symbol's count (ballot peer
+//      matching) -> per-symbol prefix over the chunks (thread = symbol),
+//      with the symbol's first x (norm, or 1 for -1) folded in -> entry of
+//      position i from x = prefix + peers below, stored coalesced.
+// ------------------------------------------------------------------------
+template <int LMAX>
+__global__ __launch_bounds__(256) void dtable_par_kernel(DtParams P) {
+    static_assert(LMAX <= 11, "ranks of 2^LMAX / 64 chunks x 256 symbols in LDS");
+    constexpr uint32_t NT = 256, NW = NT / 64u, SIZE = 1u << LMAX, NCH = SIZE / 64u;
+    __shared__ __attribute__((aligned(16))) uint8_t sym_at[SIZE];
+    __shared__ __attribute__((aligned(16))) uint8_t occ[SIZE];
+    __shared__ __attribute__((aligned(16))) uint16_t rk[NCH * 256u];
+    __shared__ uint32_t xs[4 * NW];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    const uint64_t gb = blockIdx.x;
+    if (gb >= P.n_blocks) return;
+    FSE_STAMP(P, 0);
+    const uint8_t* in = P.in + gb * P.slot_bytes;
+    const uint32_t clen = P.comp_len[gb];
+    const uint32_t last = (clen && clen <= P.slot_bytes) ? in[clen - 1u] : 0u;
+    const int2 m = P.hdr_meta[gb];
+    const int hl = m.x;
+    const uint32_t L = (uint32_t)m.y & 0xFFu, tl = (uint32_t)m.y >> 8;
+    int rc = hl < 0 ? hl : FSE_OK;
+    if (rc == FSE_OK && ((uint32_t)hl >= clen || last == 0)) rc = FSE_ERR_NO_MARKER;  // lib.rs:222
+    if (rc == FSE_OK && clen > (1u << 28)) rc = FSE_ERR_UNSUPPORTED;  // bit positions are 32-bit in the decoders
+    if (rc == FSE_OK && L > (uint32_t)LMAX) rc = FSE_ERR_UNSUPPORTED;
+    // (block-uniform from here on: every thread read the same words)
+    const uint32_t size = 1u << L, mask = size - 1u;
+    // 1. one symbol per thread
+    const uint32_t s = tid;
+    const uint32_t q = P.hdr_norm[gb * 128u + (s >> 1)];
+    const int32_t v = rc == FSE_OK && s < tl ? (int32_t)(int16_t)(q >> (16u * (s & 1u))) : 0;
+    const uint32_t neg = v < 0 ? 1u : 0u, pos = v > 0 ? (uint32_t)v : 0u;
+    const uint32_t ip = wave_incl_sum(pos), in_ = wave_incl_sum(neg);
+    if (lane == 63) {
+        xs[wv] = ip;
+        xs[NW + wv] = in_;
+    }
+    for (uint32_t i = tid; i < SIZE / 16u; i += NT) reinterpret_cast<uint4*>(occ)[i] = make_uint4(0, 0, 0, 0);
+    for (uint32_t i = tid; i < NCH * 256u / 8u; i += NT) reinterpret_cast<uint4*>(rk)[i] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    uint32_t ep = ip - pos, en = in_ - neg, total_pos = 0, total_neg = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < NW; ++w) {
+        ep += w < wv ? xs[w] : 0u;
+        en += w < wv ? xs[NW + w] : 0u;
+        total_pos += xs[w];
+        total_neg += xs[NW + w];
+    }
+    if (rc == FSE_OK && (total_pos + total_neg > size)) rc = FSE_ERR_BAD_TABLE;
+    const int32_t ht = (int32_t)size - 1 - (int32_t)total_neg;
+    if (rc == FSE_OK) {
+        if (pos) occ[ep] = (uint8_t)s;  // start mark of s's occurrences
+        if (neg) sym_at[size - 1u - en] = (uint8_t)s;  // -1 symbols from the top (fse.rs:122-125)
+    }
+    __syncthreads();
+    FSE_STAMP(P, 1);
+    // 2. forward max-fill over the occurrences, 8 per thread
+    {
+        uint2* o8 = reinterpret_cast<uint2*>(occ);
+        const bool in8 = tid * 8u < SIZE;
+        const uint2 w = in8 ? o8[tid] : make_uint2(0, 0);
+        uint32_t mx[8];
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) {
+            const uint32_t b = ((k < 4 ? w.x : w.y) >> (8u * (k & 3u))) & 0xFFu;
+            mx[k] = k ? max(mx[k - 1], b) : b;
+        }
+        const uint32_t incl = wave_incl_max(mx[7]);
+        if (lane == 63) xs[2 * NW + wv] = incl;
+        __syncthreads();
+        uint32_t carry = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < NW; ++u) carry = u < wv ? max(carry, xs[2 * NW + u]) : carry;
+        const uint32_t b = max(carry, wave_shr1(incl));
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) {
+            const uint32_t x = max(b, mx[k]) << (8u * (k & 3u));
+            if (k < 4) lo |= x; else hi |= x;
+        }
+        if (in8) o8[tid] = make_uint2(lo, hi);
+    }
+    __syncthreads();
+    FSE_STAMP(P, 2);
+    // 3. the spread walk, multipliers 8 * tid .. 8 * tid + 7 (fse.rs:139-150)
+    {
+        const uint32_t step = (size >> 3) * 5u + 3u;  // table_step (fse.rs:67-70)
+        uint32_t p[8], nv = 0;
+        bool keep[8];
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) {
+            const uint32_t mm = tid * 8u + k;
+            p[k] = (mm * step) & mask;
+            keep[k] = mm < size && (int32_t)p[k] <= ht;
+            nv += keep[k] ? 1u : 0u;
+        }
+        const uint32_t incl = wave_incl_sum(nv);
+        if (lane == 63) xs[3 * NW + wv] = incl;
+        __syncthreads();
+        uint32_t j = incl - nv, kept = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < NW; ++u) {
+            j += u < wv ? xs[3 * NW + u] : 0u;
+            kept += xs[3 * NW + u];
+        }
+        if (rc == FSE_OK && kept != total_pos) rc = FSE_ERR_BAD_TABLE;  // position != 0 assert
+        if (rc == FSE_OK) {
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k) {
+                if (keep[k] && j < total_pos) sym_at[p[k]] = occ[j];
+                j += keep[k] ? 1u : 0u;
+            }
+        }
+    }
+    __syncthreads();
+    FSE_STAMP(P, 3);
+    if (rc != FSE_OK) {
+        if (tid == 0) P.dtinfo[gb] = rc;
+        return;
+    }
+    // 4a. per chunk t (64 positions; wave wv takes t = wv, wv + NW, ...):
+    // each symbol's count, and each lane's peers below
+    const uint32_t nch = size >= 64u ? size / 64u : 1u, kb = key_bits(tl);
+    constexpr uint32_t CPW = (NCH + NW - 1u) / NW;  // chunks per wave
+    uint32_t below[CPW], sy[CPW];
+#pragma unroll
+    for (uint32_t c = 0; c < CPW; ++c) {
+        const uint32_t t = wv + c * NW;
+        below[c] = sy[c] = 0;
+        if (t < nch) {
+            const uint32_t i = t * 64u + lane;
+            const bool act = i < size;
+            sy[c] = act ? sym_at[i] : 0u;
+            const uint64_t peers = match_key(sy[c], __ballot(act), kb);
+            below[c] = (uint32_t)__popcll(peers & lanemask_lt());
+            if (act && below[c] == 0) rk[t * 256u + sy[c]] = (uint16_t)__popcll(peers);
+        }
+    }
+    __syncthreads();
+    FSE_STAMP(P, 4);
+    // 4b. per symbol (thread = symbol): prefix over the chunks, starting at
+    // the symbol's first x (fse.rs:300-306: norm, or 1 for a -1 symbol)
+    if (s < tl) {
+        uint32_t run = v < 0 ? 1u : (uint32_t)v;
+        uint16_t c[NCH];
+#pragma unroll
+        for (uint32_t t = 0; t < NCH; ++t) c[t] = t < nch ? rk[t * 256u + s] : 0;
+#pragma unroll
+        for (uint32_t t = 0; t < NCH; ++t) {
+            if (t < nch) rk[t * 256u + s] = (uint16_t)run;
+            run += c[t];
+        }
+    }
+    __syncthreads();
+    FSE_STAMP(P, 5);
+    // 4c. entries (fse.rs:329-337), one coalesced store per chunk
+    uint32_t* dt = P.dt + gb * (uint64_t)SIZE;
+#pragma unroll
+    for (uint32_t c = 0; c < CPW; ++c) {
+        const uint32_t t = wv + c * NW;
+        const uint32_t i = t * 64u + lane;
+        if (t < nch && i < size) {
+            const uint32_t nx = (uint32_t)rk[t * 256u + sy[c]] + below[c];
+            const uint32_t nb = L - ilog2u(nx);
+            dt[i] = Dte<LMAX>::make(nb, sy[c], (nx << nb) - size);
+        }
+    }
+    if (tid == 0) P.dtinfo[gb] = (int32_t)((uint32_t)hl | (L << 16));
+    FSE_STAMP(P, 8);
+}
+
+// ------------------------------------------------------------------------
 // fse_decompress (lib.rs:187-211) without a sidecar: one lane per block
 // walks the stream with every read checked, on tables from
 // dtable_blocks_kernel.  Container mode (raw length known) or the
@@ -2249,7 +2435,8 @@ hipError_t launch_dtables(const DtParams& P0, uint32_t lmax, hipStream_t stream)
         P.hdr_meta = nullptr;
     }
     const dim3 g(P.n_blocks), b(64);
-    if (lmax <= 11) hipLaunchKernelGGL((dtable_blocks_kernel<11>), g, b, P.xlds, stream, P);
+    if (lmax <= 11 && P.hdr_meta && !P.one_wave) hipLaunchKernelGGL((dtable_par_kernel<11>), g, dim3(256), P.xlds, stream, P);
+    else if (lmax <= 11) hipLaunchKernelGGL((dtable_blocks_kernel<11>), g, b, P.xlds, stream, P);
     else if (lmax <= 12) hipLaunchKernelGGL((dtable_blocks_kernel<12>), g, b, P.xlds, stream, P);
     else if (lmax <= 13) hipLaunchKernelGGL((dtable_blocks_kernel<13>), g, b, P.xlds, stream, P);
     else if (lmax <= 14) hipLaunchKernelGGL((dtable_blocks_kernel<14>), g, b, P.xlds, stream, P);

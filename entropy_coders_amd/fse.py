@@ -98,6 +98,27 @@ def decompress(src, cap: int = 1 << 24) -> bytes:
     return dst[: n.value].tobytes()
 
 
+def decompress2_many(streams, dst_stride: int, nstates: int = 2):
+    """`fse_decompress2_many` / `fse_decompress_many` (nstates 1): many crate
+    streams from host memory in one call, each decoded as `fse_decompress2`
+    (lib.rs:215) would within dst_stride bytes.  Returns a list with, per
+    stream, its bytes or the name of its status."""
+    from ._lib import STATUS
+
+    lib = load()
+    bufs = [_buf(x) for x in streams]
+    n = len(bufs)
+    ptrs = (C.c_void_p * max(n, 1))(*[b.ctypes.data if len(b) else None for b in bufs])
+    lens = (C.c_size_t * max(n, 1))(*[len(b) for b in bufs])
+    dst = np.zeros(max(n, 1) * dst_stride, dtype=np.uint8)
+    out_lens = (C.c_size_t * max(n, 1))()
+    st = (C.c_int32 * max(n, 1))()
+    fn = lib.fse_decompress2_many if nstates == 2 else lib.fse_decompress_many
+    check(fn(ptrs, lens, n, _p(dst), dst_stride, out_lens, st), "fse_decompress2_many")
+    return [dst[i * dst_stride: i * dst_stride + out_lens[i]].tobytes() if st[i] == 0 else
+            STATUS.get(int(st[i]), str(int(st[i]))) for i in range(n)]
+
+
 def decompress_streams(streams, out_stride: int, nstates: int = 2, max_table_log: int = 11, device=None):
     """`fsehip_decompress_streams`: many crate streams (no sidecar, no raw
     length) decoded at once on the GPU, each as `fse_decompress2` (nstates 2)
@@ -537,7 +558,8 @@ class BlockCodec:
 
 __all__ = ["BITS_ADVANCE", "BITS_PEEK", "BITS_READ", "BitStackReader", "BitStackWriter", "BitStreamReader", "BlockCodec", "DecodeTable", "EncodeTable", "FseError",
            "Histogram", "NormHistogram", "bitstack_read", "bitstack_write", "bitstream_read", "compress", "compress2",
-           "compress2_log", "compress_nh", "decode_table_new", "decompress", "decompress2", "decompress_streams",
+           "compress2_log", "compress_nh", "decode_table_new", "decompress", "decompress2", "decompress2_many",
+           "decompress_streams",
            "encode_table_new",
            "histogram_count", "histogram_new", "norm_histogram_new", "norm_histogram_read", "norm_histogram_write",
            "normalize", "normalize_optimal"]

@@ -63,8 +63,9 @@ int fse_compress2_log(const uint8_t* src, size_t n, uint32_t table_log, uint8_t*
  * memory (the input, and up to 4 MiB of the result; larger results come back
  * by a plain device-to-host copy) and device memory (input, output up to
  * dst_cap - *dst_len, tables).  fsehip_release_workspace frees them.  A lone
- * stream decodes as one serial chain (~1.4 ms per 64 KiB call on MI355X);
- * many streams belong on fsehip_decompress_streams. */
+ * stream decodes as one serial chain (~1.4 ms per 64 KiB call on MI355X,
+ * slower than one host core); many streams belong on fse_decompress2_many
+ * (host buffers) or fsehip_decompress_streams (device buffers). */
 int fse_decompress2(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, size_t* dst_len);
 
 /* The 1-state format: replaces `pub fn fse_compress(src, dst) -> (NormHistogram, usize)`
@@ -73,6 +74,32 @@ int fse_decompress2(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, 
  * conventions as the 2-state pair above. */
 int fse_compress(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, size_t* dst_len, uint64_t* payload_bits);
 int fse_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, size_t* dst_len);
+
+/* Many fse_decompress2 / fse_decompress calls in one (lib.rs:215-248 /
+ * 187-211 per stream): the drop-in for a caller's loop over many crate
+ * streams.  Stream i (srcs[i], src_lens[i] bytes) decodes into
+ * dst + i * dst_stride with at most dst_stride bytes; dst_lens[i] = bytes
+ * decoded and statuses[i] = its status, as the single call would return it
+ * (EMPTY, BAD_HEADER, NO_MARKER, TOO_SHORT, SINGLE_SYMBOL, DST_TOO_SMALL,
+ * UNSUPPORTED above 2^28 bytes).  Returns FSE_OK when the batch ran (look at
+ * statuses), or a call-level error (BAD_ARG, NO_DEVICE, HIP).
+ *
+ * Where the GPU pays.  A lone stream is one serial chain: fse_decompress2
+ * takes ~1.4 ms per 64 KiB call on MI355X against ~0.14-0.4 ms on one host
+ * core, so the per-call path never beats a CPU core.  This call stages all
+ * streams through pinned memory in one copy each way and decodes them as
+ * thousands of chains at once (fsehip_decompress_streams): its time is ~a
+ * fixed 3-4 ms per round of up to ~8,000 64 KiB streams plus the PCIe copies,
+ * so it beats one host core from a few dozen 64 KiB streams and 16 cores
+ * from a few hundred (tools/many_streams.py measures the crossover;
+ * bench.py's host_call_latency reports 1,000 streams).  One or two streams
+ * take the single-stream path.  Synchronous on the default stream; the
+ * staging buffers are per thread (grow-only, freed by
+ * fsehip_release_workspace). */
+int fse_decompress2_many(const uint8_t* const* srcs, const size_t* src_lens, size_t n_streams, uint8_t* dst,
+                         size_t dst_stride, size_t* dst_lens, int32_t* statuses);
+int fse_decompress_many(const uint8_t* const* srcs, const size_t* src_lens, size_t n_streams, uint8_t* dst,
+                        size_t dst_stride, size_t* dst_lens, int32_t* statuses);
 
 /* Replaces `Histogram::new(data)` (histogram.rs:18-66) -- the north star's
  * `histogram::count`: counts[256], table_len = 1 + largest symbol. */

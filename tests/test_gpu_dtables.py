@@ -200,3 +200,53 @@ def test_dtables_damaged_headers(torch_cuda, n_blocks):
         assert np.array_equal(e & 0xFF, nb) and np.array_equal((e >> 8) & 0xFF, sym), b
         assert np.array_equal(e >> 18, ns), b
     # (damaged headers often still parse: the oracle then gives the same other table)
+
+
+@pytest.mark.parametrize("log2", [0, 5, 6, 8, 10, 11])
+def test_dtables_parallel_build_match_oracle(torch_cuda, log2):
+    """Batches of >= 256 blocks at L <= 11 build their tables with the
+    4-wave kernel (dtable_par_kernel) from the lane-parallel header parse:
+    every block's table against the oracle's DecodeTable entry for entry,
+    over skewed / near-uniform (table_len > 64) / sparse / geometric blocks,
+    so -1 symbols, long zero runs and wide alphabets all occur."""
+    torch = torch_cuda
+    from entropy_coders_amd import BlockCodec
+
+    rng = np.random.default_rng(0x9A2 + log2)
+    nb_, bs = 288, 4096
+    blocks = []
+    for b in range(nb_):
+        k = b % 4
+        if k == 0:
+            blocks.append(O.generate(0, float(rng.uniform(0.05, 0.8)), int(rng.integers(1 << 30)), b, bs))
+        elif k == 1:
+            blocks.append(O.generate(2, 0.0, int(rng.integers(1 << 30)), b, bs))
+        elif k == 2:
+            alpha = np.sort(rng.choice(256, size=int(rng.integers(2, 120)), replace=False)).astype(np.uint8)
+            w = rng.random(len(alpha)) ** 4 + 1e-4
+            blocks.append(alpha[rng.choice(len(alpha), size=bs, p=w / w.sum())])
+        else:
+            blocks.append(np.minimum(rng.geometric(float(rng.uniform(0.2, 0.8)), bs) - 1, 255).astype(np.uint8))
+    host = np.concatenate(blocks)
+    codec = BlockCodec(block_size=bs, table_log=log2, ckpt_interval=64)
+    cb = codec.compress(torch.from_numpy(host).cuda())
+    tabs = codec.build_dtables(cb)
+    torch.cuda.synchronize()
+    st = cb["status"].cpu().numpy()
+    info = tabs["info"].cpu().numpy()
+    per = int(codec.lib.fsehip_dtable_bytes(codec.max_table_log)) // 4
+    dt = tabs["dt"].cpu().numpy().view(np.uint32)
+    checked = wide = 0
+    for b in range(nb_):
+        if st[b] != 0:  # e.g. a single-symbol block at a forced log
+            continue
+        blk = codec.block_bytes(cb, b)
+        L, ns, sym, nb, used = O.dtable(blk)
+        assert info[b] >= 0 and info[b] >> 16 == L and info[b] & 0xFFFF == used, (b, info[b])
+        e = dt[b * per: b * per + (1 << L)]
+        assert np.array_equal(e & 0xFF, nb), b
+        assert np.array_equal((e >> 8) & 0xFF, sym), b
+        assert np.array_equal(e >> 18, ns), b
+        checked += 1
+        wide += int(sym.max()) >= 64
+    assert checked >= nb_ * 3 // 4 and wide > 0, (checked, wide)

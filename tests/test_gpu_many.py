@@ -1,0 +1,97 @@
+"""The batching drop-in for a caller with many crate streams:
+fse_decompress2_many / fse_decompress_many (include/fsehip.h) through the
+C ABI (ctypes), 1,000 crate-format streams per call, each checked against
+the oracle's fse_decompress2 / fse_decompress (lib.rs:215-248 / 187-211):
+bytes for the good streams, the status name for damaged and degenerate
+ones (reference mode, within the stride)."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def _streams(rng, n, nstates):
+    streams = []
+    for i in range(n):
+        size = int(rng.choice([65536, 65536, int(rng.integers(2, 65537))]))
+        kind = i % 5
+        if kind == 0:
+            src = O.generate(0, 0.155, 0x5EED0002, i, size)  # the bench's C2 data
+        elif kind == 1:
+            src = O.generate(0, float(rng.uniform(0.05, 0.8)), int(rng.integers(1 << 30)), 0, size)
+        elif kind == 2:
+            alpha = rng.choice(256, size=int(rng.integers(2, 200)), replace=False).astype(np.uint8)
+            src = alpha[rng.integers(0, len(alpha), size)]
+        elif kind == 3:
+            src = np.minimum(rng.geometric(0.5, size) - 1, 255).astype(np.uint8)  # C1's shape
+        else:
+            src = rng.integers(0, 256, size).astype(np.uint8)
+        try:
+            if nstates == 2:
+                L = int(rng.choice([0, 0, 0, 9, 10, 12]))
+                comp = O.compress2(src, L or None)[0]
+            else:
+                comp = O.compress(src)[0]
+        except O.OracleError:
+            continue
+        comp = bytearray(comp)
+        if i % 97 == 13:  # damaged
+            comp[int(rng.integers(0, len(comp)))] ^= 0x3C
+        if i % 211 == 7:  # truncated
+            comp = comp[: max(1, len(comp) // 3)]
+        streams.append(bytes(comp))
+    streams.append(b"")  # EMPTY, as the single call returns it
+    return streams
+
+
+@pytest.mark.parametrize("nstates", [2, 1])
+def test_many_streams_exact(torch_cuda, nstates):
+    from entropy_coders_amd import decompress2_many
+
+    rng = np.random.default_rng(0x4A11 + nstates)
+    streams = _streams(rng, 1000, nstates)
+    stride = 65536
+    got = decompress2_many(streams, stride, nstates=nstates)
+    ref = O.decompress2 if nstates == 2 else O.decompress
+    n_ok = n_err = 0
+    for i, (x, g) in enumerate(zip(streams, got)):
+        try:
+            want = ref(x, stride) if x else None
+        except O.OracleError as e:
+            assert g == e.code, (i, e.code, g)
+            n_err += 1
+            continue
+        if want is None:
+            assert g == "EMPTY", (i, g)
+            continue
+        assert g == want, i
+        n_ok += 1
+    assert n_ok >= 950 and n_err >= 1 and n_ok + n_err == len(streams) - 1, (n_ok, n_err)
+
+
+def test_many_streams_short_stride_and_small_batches(torch_cuda):
+    """DST_TOO_SMALL per stream when the stride is short, and the one- and
+    two-stream batches (which take the single-stream path) agree with the
+    batch path."""
+    from entropy_coders_amd import decompress2, decompress2_many
+
+    srcs = [O.generate(0, 0.155, 0x5EED0002, i, 65536) for i in range(5)]
+    comps = [O.compress2(s)[0] for s in srcs]
+    got = decompress2_many(comps, 40000)
+    assert got == ["DST_TOO_SMALL"] * 5
+    for k in (1, 2, 3):
+        got = decompress2_many(comps[:k], 65536)
+        assert got == [s.tobytes() for s in srcs[:k]]
+    assert decompress2_many([], 16) == []
+    assert decompress2(comps[0]) == srcs[0].tobytes()
