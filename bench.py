@@ -319,7 +319,9 @@ def host_call_latency(reps: int = 20) -> dict:
     if decompress2_many(many[:8], 65536) != [O.generate(0, 0.155, 0x5EED0002, i, 65536).tobytes()
                                              for i in range(8)]:
         raise RuntimeError("fse_decompress2_many differs from the source")
-    t_many = med_us(lambda: decompress2_many(many, 65536))
+    many_np = [np.frombuffer(c, dtype=np.uint8) for c in many]
+    many_dst = np.empty(len(many) * 65536, dtype=np.uint8)
+    t_many = med_us(lambda: decompress2_many(many_np, 65536, raw=True, dst=many_dst))
     t_one = med_us(lambda: [O.decompress2(c, cap) for c in many[:32]]) / 32
     return {"workload": "one 64 KiB C2 block per call (host buffers in and out), median of "
                         f"{reps} calls; oracle = the C restatement on one host core",
@@ -429,7 +431,7 @@ def load_traffic(name: str):
         return None
 
 
-def roofline_lds(kernel: str, ms: float, profiled: bool = True):
+def roofline_lds(kernel: str, ms: float, profiled: bool = True, alg_bytes: int = 0):
     """LDS-side roofline of a kernel whose launch took `ms` (HIP events, this
     run): its LDS-array cycles per launch summed over the CUs (rocprofv3
     SQ_LDS_IDX_ACTIVE, profiles/lds.json from tools/lds_pass.sh +
@@ -451,12 +453,21 @@ def roofline_lds(kernel: str, ms: float, profiled: bool = True):
     cycles = ms * 1e-3 * clk * 1e9 * doc.get("cus", 256)
     busy = k["lds_array_cycles_per_launch"] / cycles
     useful = (k["lds_array_cycles_per_launch"] - k["bank_conflict_cycles_per_launch"]) / cycles
-    return {"bound": "lds", "kernel": kernel, "unit": "LDS-array cycles per CU-cycle", "achieved": round(busy, 4),
-            "peak": 1.0, "frac": round(busy, 4), "useful_frac": round(useful, 4),
-            "conflict_share": round(k["bank_conflict_cycles_per_launch"] / max(k["lds_array_cycles_per_launch"], 1), 4),
-            "lds_array_cycles_per_launch": k["lds_array_cycles_per_launch"], "clock_ghz": clk,
-            "source": "profiles/lds.json: rocprofv3 SQ_LDS_IDX_ACTIVE / SQ_LDS_BANK_CONFLICT / GRBM_GUI_ACTIVE per "
-                      "launch (tools/lds_pass.sh, tools/lds_summary.py); time = this run's HIP events"}
+    out = {"bound": "lds", "kernel": kernel, "unit": "LDS-array cycles per CU-cycle", "achieved": round(busy, 4),
+           "peak": 1.0, "frac": round(busy, 4), "useful_frac": round(useful, 4),
+           "conflict_share": round(k["bank_conflict_cycles_per_launch"] / max(k["lds_array_cycles_per_launch"], 1), 4),
+           "lds_array_cycles_per_launch": k["lds_array_cycles_per_launch"], "clock_ghz": clk,
+           "source": "profiles/lds.json: rocprofv3 SQ_LDS_IDX_ACTIVE / SQ_LDS_BANK_CONFLICT / GRBM_GUI_ACTIVE per "
+                     "launch (tools/lds_pass.sh, tools/lds_summary.py); time = this run's HIP events"}
+    # the launch can take no less than its LDS-array cycles at one per CU-cycle:
+    # the HBM-roofline fraction this design could reach with the LDS 100 % busy
+    min_ms = k["lds_array_cycles_per_launch"] / (doc.get("cus", 256) * clk * 1e9) * 1e3
+    out["min_ms_at_full_lds"] = round(min_ms, 4)
+    if alg_bytes:
+        out["ceiling_hbm_frac"] = round(alg_bytes / (min_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    if k.get("split"):
+        out["split"] = k["split"]
+    return out
 
 
 def roofline(kernel: str, ms: float, alg_bytes: int, what: str, profiled: bool = True) -> dict:
@@ -614,7 +625,7 @@ def main():
                                         "decode-table + decode launches, HIP events", prof_cfg),
             # the encoder is bound by its LDS (random table gathers, histogram
             # atomics), not by HBM: its LDS-array occupancy beside the HBM line
-            "roofline_lds": roofline_lds("fse_encode_blocks", enc_ms, prof_cfg),
+            "roofline_lds": roofline_lds("fse_encode_blocks", enc_ms, prof_cfg, enc_bytes),
             "encode_ms": round(enc_ms, 4),
             "decode_ms": round(dec_ms, 4),
             "encode_GiB_s": round(n / (enc_ms * 1e-3) / 2**30, 2),
@@ -729,7 +740,8 @@ def main():
               # the same launch priced on the reference format's bytes only
               # (compressed read + raw written; the sidecar is this port's own)
               "frac_reference_format_bytes": round((comp3 + n3) / (c3_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-              "roofline_lds": roofline_lds("fse_decode_blocks_c3", c3_ms, prof_base and args.c3_blocks == 32768),
+              "roofline_lds": roofline_lds("fse_decode_blocks_c3", c3_ms, prof_base and args.c3_blocks == 32768,
+                                           c3_bytes),
               "verified": c3_ok}
         ok = ok and c3_ok
         del src3, cb3, tabs, out3, st3

@@ -542,7 +542,7 @@ static int build_dtables_impl(const fsehip_params* p, const uint8_t* d_in, uint6
     D.dt = d_dtables;
     D.dtinfo = d_dtinfo;
     D.xlds = env_u32("FSEHIP_DT_XLDS", 0);  // diagnostics: occupancy probe
-    D.one_wave = env_u32("FSEHIP_DT_ONE_WAVE", 0);  // diagnostics: A/B of the table kernels
+    D.par = env_u32("FSEHIP_DT_PAR", 0);  // diagnostics: the 4-wave table kernel (A/B)
     D.stamps = g_stamps_dt.get(n_blocks);
     hipError_t e = fsehip::launch_dtables(D, kern_lmax(p->max_table_log), static_cast<hipStream_t>(stream));
     if (D.stamps) g_stamps_dt.report("dtables", n_blocks, static_cast<hipStream_t>(stream));

@@ -987,6 +987,13 @@ __global__ __launch_bounds__(64) void dtable_blocks_kernel(DtParams P) {
 //      with the symbol's first x (norm, or 1 for -1) folded in -> entry of
 //      position i from x = prefix + peers below, stored coalesced.
 // ------------------------------------------------------------------------
+// Measured slower than the one-wave kernel on C2 (0.132 vs 0.100 ms with
+// the header parse; profiles/r05/dtable_par/): 19.3K cycles per table at 7
+// workgroups per CU (its 16 KB rank table) against ~60K at 21 one-wave
+// workgroups per CU -- the ballot peer matching of pass 1 (6.4K) and the
+// dependent loads of step 1 (5.1K) keep the latency up.  Diagnostics build
+// only (FSEHIP_DT_PAR=1), kept as the recorded alternative.
+#if FSEHIP_DIAG
 template <int LMAX>
 __global__ __launch_bounds__(256) void dtable_par_kernel(DtParams P) {
     static_assert(LMAX <= 11, "ranks of 2^LMAX / 64 chunks x 256 symbols in LDS");
@@ -1005,9 +1012,9 @@ __global__ __launch_bounds__(256) void dtable_par_kernel(DtParams P) {
     const int2 m = P.hdr_meta[gb];
     const int hl = m.x;
     const uint32_t L = (uint32_t)m.y & 0xFFu, tl = (uint32_t)m.y >> 8;
+    // the header's own status gates the build; the marker and length checks
+    // (lib.rs:222) wait for the marker byte's load, which lands meanwhile
     int rc = hl < 0 ? hl : FSE_OK;
-    if (rc == FSE_OK && ((uint32_t)hl >= clen || last == 0)) rc = FSE_ERR_NO_MARKER;  // lib.rs:222
-    if (rc == FSE_OK && clen > (1u << 28)) rc = FSE_ERR_UNSUPPORTED;  // bit positions are 32-bit in the decoders
     if (rc == FSE_OK && L > (uint32_t)LMAX) rc = FSE_ERR_UNSUPPORTED;
     // (block-uniform from here on: every thread read the same words)
     const uint32_t size = 1u << L, mask = size - 1u;
@@ -1100,23 +1107,32 @@ __global__ __launch_bounds__(256) void dtable_par_kernel(DtParams P) {
     }
     __syncthreads();
     FSE_STAMP(P, 3);
+    // after the header's status and before the table's, as the one-wave kernel orders them
+    if (hl >= 0 && L <= (uint32_t)LMAX) {
+        if ((uint32_t)hl >= clen || last == 0) rc = FSE_ERR_NO_MARKER;  // lib.rs:222
+        else if (clen > (1u << 28)) rc = FSE_ERR_UNSUPPORTED;  // bit positions are 32-bit in the decoders
+    }
     if (rc != FSE_OK) {
         if (tid == 0) P.dtinfo[gb] = rc;
         return;
     }
     // 4a. per chunk t (64 positions; wave wv takes t = wv, wv + NW, ...):
-    // each symbol's count, and each lane's peers below
+    // each symbol's count, and each lane's peers below (the chunks' symbols
+    // are read first, all in flight at once)
     const uint32_t nch = size >= 64u ? size / 64u : 1u, kb = key_bits(tl);
     constexpr uint32_t CPW = (NCH + NW - 1u) / NW;  // chunks per wave
     uint32_t below[CPW], sy[CPW];
 #pragma unroll
     for (uint32_t c = 0; c < CPW; ++c) {
+        const uint32_t i = (wv + c * NW) * 64u + lane;
+        sy[c] = i < size ? sym_at[i] : 0u;
+    }
+#pragma unroll
+    for (uint32_t c = 0; c < CPW; ++c) {
         const uint32_t t = wv + c * NW;
-        below[c] = sy[c] = 0;
+        below[c] = 0;
         if (t < nch) {
-            const uint32_t i = t * 64u + lane;
-            const bool act = i < size;
-            sy[c] = act ? sym_at[i] : 0u;
+            const bool act = t * 64u + lane < size;
             const uint64_t peers = match_key(sy[c], __ballot(act), kb);
             below[c] = (uint32_t)__popcll(peers & lanemask_lt());
             if (act && below[c] == 0) rk[t * 256u + sy[c]] = (uint16_t)__popcll(peers);
@@ -1154,6 +1170,7 @@ __global__ __launch_bounds__(256) void dtable_par_kernel(DtParams P) {
     if (tid == 0) P.dtinfo[gb] = (int32_t)((uint32_t)hl | (L << 16));
     FSE_STAMP(P, 8);
 }
+#endif  // FSEHIP_DIAG
 
 // ------------------------------------------------------------------------
 // fse_decompress (lib.rs:187-211) without a sidecar: one lane per block
@@ -2435,8 +2452,11 @@ hipError_t launch_dtables(const DtParams& P0, uint32_t lmax, hipStream_t stream)
         P.hdr_meta = nullptr;
     }
     const dim3 g(P.n_blocks), b(64);
-    if (lmax <= 11 && P.hdr_meta && !P.one_wave) hipLaunchKernelGGL((dtable_par_kernel<11>), g, dim3(256), P.xlds, stream, P);
-    else if (lmax <= 11) hipLaunchKernelGGL((dtable_blocks_kernel<11>), g, b, P.xlds, stream, P);
+#if FSEHIP_DIAG
+    if (lmax <= 11 && P.hdr_meta && P.par) hipLaunchKernelGGL((dtable_par_kernel<11>), g, dim3(256), P.xlds, stream, P);
+    else
+#endif
+    if (lmax <= 11) hipLaunchKernelGGL((dtable_blocks_kernel<11>), g, b, P.xlds, stream, P);
     else if (lmax <= 12) hipLaunchKernelGGL((dtable_blocks_kernel<12>), g, b, P.xlds, stream, P);
     else if (lmax <= 13) hipLaunchKernelGGL((dtable_blocks_kernel<13>), g, b, P.xlds, stream, P);
     else if (lmax <= 14) hipLaunchKernelGGL((dtable_blocks_kernel<14>), g, b, P.xlds, stream, P);

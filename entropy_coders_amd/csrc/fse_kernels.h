@@ -76,9 +76,9 @@ struct DtParams {
     // status, L | table_len << 8}; hdr_norm[b] = 256 x int16 counts (128 words).
     int2* hdr_meta;
     uint32_t* hdr_norm;
-    // diagnostics (FSEHIP_DT_ONE_WAVE): with hdr_meta at L <= 11, the one-wave
-    // table kernel instead of the 4-wave one (A/B runs)
-    uint32_t one_wave;
+    // diagnostics build only (FSEHIP_DT_PAR=1): with hdr_meta at L <= 11, the
+    // 4-wave table kernel (dtable_par_kernel, a measured negative) instead
+    uint32_t par;
 };
 constexpr uint64_t hdr_scratch_bytes(uint64_t n_blocks) { return n_blocks * (512u + 8u); }
 

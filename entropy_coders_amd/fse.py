@@ -98,24 +98,29 @@ def decompress(src, cap: int = 1 << 24) -> bytes:
     return dst[: n.value].tobytes()
 
 
-def decompress2_many(streams, dst_stride: int, nstates: int = 2):
+def decompress2_many(streams, dst_stride: int, nstates: int = 2, raw: bool = False, dst=None):
     """`fse_decompress2_many` / `fse_decompress_many` (nstates 1): many crate
     streams from host memory in one call, each decoded as `fse_decompress2`
     (lib.rs:215) would within dst_stride bytes.  Returns a list with, per
-    stream, its bytes or the name of its status."""
+    stream, its bytes or the name of its status; with raw=True the call's own
+    outputs instead: (dst, lengths, statuses) as numpy arrays (dst may be
+    passed in, n * dst_stride bytes, to reuse one buffer across calls)."""
     from ._lib import STATUS
 
     lib = load()
     bufs = [_buf(x) for x in streams]
     n = len(bufs)
-    ptrs = (C.c_void_p * max(n, 1))(*[b.ctypes.data if len(b) else None for b in bufs])
-    lens = (C.c_size_t * max(n, 1))(*[len(b) for b in bufs])
-    dst = np.zeros(max(n, 1) * dst_stride, dtype=np.uint8)
-    out_lens = (C.c_size_t * max(n, 1))()
-    st = (C.c_int32 * max(n, 1))()
+    ptrs = np.array([b.ctypes.data if len(b) else 0 for b in bufs] or [0], dtype=np.uintp)
+    lens = np.array([len(b) for b in bufs] or [0], dtype=np.uintp)
+    if dst is None:
+        dst = np.empty(max(n, 1) * dst_stride, dtype=np.uint8)
+    out_lens = np.zeros(max(n, 1), dtype=np.uintp)
+    st = np.zeros(max(n, 1), dtype=np.int32)
     fn = lib.fse_decompress2_many if nstates == 2 else lib.fse_decompress_many
-    check(fn(ptrs, lens, n, _p(dst), dst_stride, out_lens, st), "fse_decompress2_many")
-    return [dst[i * dst_stride: i * dst_stride + out_lens[i]].tobytes() if st[i] == 0 else
+    check(fn(_p(ptrs), _p(lens), n, _p(dst), dst_stride, _p(out_lens), _p(st)), "fse_decompress2_many")
+    if raw:
+        return dst, out_lens[:n], st[:n]
+    return [dst[i * dst_stride: i * dst_stride + int(out_lens[i])].tobytes() if st[i] == 0 else
             STATUS.get(int(st[i]), str(int(st[i]))) for i in range(n)]
 
 

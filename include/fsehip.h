@@ -88,12 +88,12 @@ int fse_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, s
  * takes ~1.4 ms per 64 KiB call on MI355X against ~0.14-0.4 ms on one host
  * core, so the per-call path never beats a CPU core.  This call stages all
  * streams through pinned memory in one copy each way and decodes them as
- * thousands of chains at once (fsehip_decompress_streams): its time is ~a
- * fixed 3-4 ms per round of up to ~8,000 64 KiB streams plus the PCIe copies,
- * so it beats one host core from a few dozen 64 KiB streams and 16 cores
- * from a few hundred (tools/many_streams.py measures the crossover;
- * bench.py's host_call_latency reports 1,000 streams).  One or two streams
- * take the single-stream path.  Synchronous on the default stream; the
+ * thousands of chains at once (fsehip_decompress_streams): 2.6 ms for 16
+ * 64 KiB streams, 3.7 ms for 256, 6.3 ms for 1,000 (9.7 GiB/s), 16.5 ms for
+ * 4,000 (14.8 GiB/s), PCIe included, so it beats one host core from ~16
+ * streams and 16 cores from ~256 (tools/many_streams.py; bench.py's
+ * host_call_latency reports 1,000 streams).  One or two streams take the
+ * single-stream path.  Synchronous on the default stream; the
  * staging buffers are per thread (grow-only, freed by
  * fsehip_release_workspace). */
 int fse_decompress2_many(const uint8_t* const* srcs, const size_t* src_lens, size_t n_streams, uint8_t* dst,

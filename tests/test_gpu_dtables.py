@@ -204,11 +204,12 @@ def test_dtables_damaged_headers(torch_cuda, n_blocks):
 
 @pytest.mark.parametrize("log2", [0, 5, 6, 8, 10, 11])
 def test_dtables_parallel_build_match_oracle(torch_cuda, log2):
-    """Batches of >= 256 blocks at L <= 11 build their tables with the
-    4-wave kernel (dtable_par_kernel) from the lane-parallel header parse:
+    """Batches of >= 256 blocks at L <= 11 build their tables from the
+    lane-parallel header parse (hdr_parse_kernel -> dtable_blocks_kernel):
     every block's table against the oracle's DecodeTable entry for entry,
     over skewed / near-uniform (table_len > 64) / sparse / geometric blocks,
-    so -1 symbols, long zero runs and wide alphabets all occur."""
+    so -1 symbols, long zero runs and wide alphabets all occur.  (The same
+    test passed on the 4-wave dtable_par_kernel of the diagnostics build.)"""
     torch = torch_cuda
     from entropy_coders_amd import BlockCodec
 

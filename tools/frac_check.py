@@ -40,6 +40,7 @@ def main():
     out.append(("encode", n, enc, alg / enc / 1e6 / PEAK, line["roofline"]["frac"]))
     hp, _ = avg(r, "hdr_parse_kernel<11>", nb // 16)
     dt, _ = avg(r, "dtable_blocks_kernel<11>", nb)
+    dt = dt or avg(r, "dtable_par_kernel<11>", nb)[0]
     dp, n = avg(r, "decode_pre_kernel<11, 45056u, 2, 1, 512u>", nb)
     rd = line["roofline_decode"]
     dec = hp + dt + dp

