@@ -184,7 +184,15 @@ struct Ckpt {
     uint64_t q[CKQ];  // q[0] = the latest entry (lowest index)
 };
 
-enum { PASS_COUNT = 1, PASS_EMIT = 2, PASS_REPAIR = 3 };
+enum { PASS_COUNT = 1, PASS_EMIT = 2, PASS_REPAIR = 3, PASS_ECOUNT = 4, PASS_EREPAIR = 5 };
+// PASS_ECOUNT / PASS_EREPAIR: the count and repair passes doing the emit
+// pass's bit packing and ring writes as well (timing probe FSEHIP_ENC_ABL & 2
+// only: the cost of an "emit from the guessed start, repair by re-emitting"
+// encoder, without its placement pass)
+template <int MODE>
+constexpr bool emits() { return MODE == PASS_EMIT || MODE == PASS_ECOUNT || MODE == PASS_EREPAIR; }
+template <int MODE>
+constexpr bool counts() { return MODE == PASS_COUNT || MODE == PASS_REPAIR || MODE == PASS_ECOUNT || MODE == PASS_EREPAIR; }
 
 // Trajectory of a count pass, for convergence-based repair: the state pair
 // and running bit count after every ckc-th chunk (at most TRACK_SLOTS slots per lane,
@@ -249,13 +257,13 @@ __device__ __forceinline__ void enc_chunk(const uint4& q, uint32_t c8, uint32_t 
             const uint32_t v0 = x0;
             const uint32_t nb0 = (t.x + x0) >> 16;
             x0 = st_at(((x0 >> nb0) << 1) + t.y);
-            if (MODE == PASS_COUNT || MODE == PASS_REPAIR) bits += nb0;
-            if (MODE == PASS_EMIT) {
+            if (counts<MODE>()) bits += nb0;
+            if (emits<MODE>()) {
                 em.put(__builtin_amdgcn_ubfe(v0, 0u, nb0), nb0);
                 if (j & 1) em.flush();  // <= 2 x 12 bits between flushes
             }
         }
-        if (MODE == PASS_EMIT) em.flush();
+        if (emits<MODE>()) em.flush();
         return;
     }
 #pragma unroll
@@ -266,8 +274,8 @@ __device__ __forceinline__ void enc_chunk(const uint4& q, uint32_t c8, uint32_t 
         x1 = st_at(((x1 >> nb1) << 1) + t1[j].y);
         const uint32_t nb0 = (t0[j].x + x0) >> 16;
         x0 = st_at(((x0 >> nb0) << 1) + t0[j].y);
-        if (MODE == PASS_COUNT || MODE == PASS_REPAIR) bits += nb1 + nb0;
-        if (MODE == PASS_EMIT) {
+        if (counts<MODE>()) bits += nb1 + nb0;
+        if (emits<MODE>()) {
             const uint32_t pairbits = (__builtin_amdgcn_ubfe(v0, 0u, nb0) << nb1) | __builtin_amdgcn_ubfe(v1, 0u, nb1);
             em.put(pairbits, nb1 + nb0);
             em.flush();
@@ -312,7 +320,8 @@ __device__ __forceinline__ void ckpt_flush(const Ckpt& ck) {
 template <int MODE, int NS>
 __device__ __forceinline__ EncState enc_range(const uint8_t* __restrict__ blk, uint32_t n, uint32_t pa, uint32_t pb,
                                               EncState st, const EncTab& T, Emit& em, Ckpt& ck, Track& tr) {
-    constexpr bool TRACK = MODE == PASS_COUNT || MODE == PASS_REPAIR;
+    constexpr bool TRACK = counts<MODE>();
+    constexpr bool RP = MODE == PASS_REPAIR || MODE == PASS_EREPAIR;
     uint32_t x0 = st.x0, x1 = st.x1, bits = st.bits;
     if (pb <= pa) return st;
     const uint4* v = reinterpret_cast<const uint4*>(blk);
@@ -328,7 +337,7 @@ __device__ __forceinline__ EncState enc_range(const uint8_t* __restrict__ blk, u
     auto track = [&]() {
         if (rem == 0u) {
             const uint32_t sv = x0 | (x1 << 16);
-            if (MODE == PASS_REPAIR) {
+            if (RP) {
                 const uint2 r = tr.cp[slot];
                 if (r.x == sv) {
                     tr.done = true;
@@ -349,23 +358,23 @@ __device__ __forceinline__ EncState enc_range(const uint8_t* __restrict__ blk, u
     if (pb & ((1u << CS) - 1u)) {  // partial topmost chunk
         const uint4 q = load_chunk(blk, n, (uint32_t)c_hi);
         enc_chunk<MODE, false, NS>(q, (uint32_t)c_hi << CS, pb, x0, x1, T, bits, em);
-        if (MODE == PASS_EMIT) em.drain();
+        if (emits<MODE>()) em.drain();
         if (MODE == PASS_EMIT && ck.base && (((uint32_t)c_hi << CS) & ck.mask) == 0u)
             ckpt_record<NS>(ck, (uint32_t)c_hi << CS, em.pos(), x0, x1);
         if (TRACK) track();
         c_hi -= 1;
     }
-    if (c_hi < c_lo || (MODE == PASS_REPAIR && tr.done)) return EncState{x0, x1, bits};
+    if (c_hi < c_lo || (RP && tr.done)) return EncState{x0, x1, bits};
     auto ld = [&](int32_t c) { return v[c < c_lo ? c_lo : c]; };
     uint4 q0 = ld(c_hi), q1 = ld(c_hi - 1), q2 = ld(c_hi - 2), q3 = ld(c_hi - 3);
     auto body = [&](const uint4& q, int32_t c) {
         enc_chunk<MODE, true, NS>(q, (uint32_t)c << CS, pb, x0, x1, T, bits, em);
-        if (MODE == PASS_EMIT) em.drain();
+        if (emits<MODE>()) em.drain();
         if (MODE == PASS_EMIT && ck.base && (((uint32_t)c << CS) & ck.mask) == 0u)
             ckpt_record<NS>(ck, (uint32_t)c << CS, em.pos(), x0, x1);
         if (TRACK) track();
     };
-    auto stop = [&](int32_t cn) { return cn < c_lo || (MODE == PASS_REPAIR && tr.done); };
+    auto stop = [&](int32_t cn) { return cn < c_lo || (RP && tr.done); };
     for (int32_t c = c_hi;; c -= 4) {
         body(q0, c);
         if (stop(c - 1)) break;
@@ -464,6 +473,9 @@ struct EncSmem {
             uint32_t mval[BPW][2 * (T + 1)];
         } p2;
     } ph;
+#if FSEHIP_ENC_ABL & 2
+    uint32_t ring2[64 * RING_STRIDE];  // the probe's count / repair emit ring
+#endif
     int32_t info_status[BPW];
     uint32_t info_L[BPW];
     uint32_t info_hl[BPW];
@@ -626,9 +638,15 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
         // odd-length extra step), every other lane from a guessed start state,
         // recording its trajectory.  Then verify against the neighbour's end
         // state and repair by convergence (Track) until the fixed point.
+#if FSEHIP_ENC_ABL & 2
+        constexpr int MC = PASS_ECOUNT, MR = PASS_EREPAIR;
+        em.start(nullptr, pa * 24u, 0u, &sm.ring2[lane * RING_STRIDE]);
+#else
+        constexpr int MC = PASS_COUNT, MR = PASS_REPAIR;
+#endif
         if (act) {
             EncState e0 = (k == ktop) ? top_start<PASS_COUNT, NS>(blk, n, tab, em) : EncState{start & 0xFFFFu, start >> 16, 0u};
-            e0 = enc_range<PASS_COUNT, NS>(blk, n, pa, pb, e0, tab, em, ck, tr);
+            e0 = enc_range<MC, NS>(blk, n, pa, pb, e0, tab, em, ck, tr);
             bits = e0.bits;
             sm.ph.p2.cntF[b][k] = e0.x0 | (e0.x1 << 16);
             track_fixup(tr, nslot, -1, bits);
@@ -650,7 +668,10 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
             if (bad) {
                 start = nbF;
                 tr.done = false;
-                const EncState e0 = enc_range<PASS_REPAIR, NS>(blk, n, pa, pb, EncState{start & 0xFFFFu, start >> 16, 0u},
+#if FSEHIP_ENC_ABL & 2
+                em.start(nullptr, pa * 24u, 0u, &sm.ring2[lane * RING_STRIDE]);
+#endif
+                const EncState e0 = enc_range<MR, NS>(blk, n, pa, pb, EncState{start & 0xFFFFu, start >> 16, 0u},
                                                            tab, em, ck, tr);
                 bits = e0.bits;
                 if (!tr.done) sm.ph.p2.cntF[b][k] = e0.x0 | (e0.x1 << 16);  // did not converge: new end state
@@ -675,7 +696,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     }
     const uint32_t total_bits = hdr_bits + __shfl(suffix, 0, T);
     const uint32_t off = hdr_bits + suffix - mybits;
-    const bool fits = (uint64_t)total_bits <= P.slot_bytes * 8ull && !(P.debug & 2u);
+    const bool fits = (uint64_t)total_bits <= P.slot_bytes * 8ull && !(P.debug & 2u) && !(FSEHIP_ENC_ABL & 2);
     uint32_t* gw = reinterpret_cast<uint32_t*>(P.out + gb * P.slot_bytes);
 
     // emit pass
