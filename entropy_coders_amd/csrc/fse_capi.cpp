@@ -866,12 +866,17 @@ static void for_streams(size_t n, uint64_t bytes, Fn fn) {
         return;
     }
     std::vector<std::thread> th;
-    th.reserve(T - 1);
     auto range = [&](size_t t) {
         for (size_t i = n * t / T; i < n * (t + 1) / T; ++i) fn(i);
     };
-    for (size_t t = 1; t < T; ++t) th.emplace_back(range, t);
+    size_t started = 1;  // ranges handed to threads (range 0 runs here)
+    try {
+        th.reserve(T - 1);
+        for (; started < T; ++started) th.emplace_back(range, started);
+    } catch (...) {  // no thread to be had (resource limits): the rest runs here
+    }
     range(0);
+    for (size_t t = started; t < T; ++t) range(t);
     for (auto& x : th) x.join();
 }
 }  // extern "C++"
