@@ -180,11 +180,22 @@ def test_decompress_streams_regressions(torch_cuda, seed):
     _streams_case(1, seed, draw=1)
 
 
-def _streams_case(nstates, seed, draw):
+@pytest.mark.parametrize("rep", range(int(os.environ.get("FSEHIP_FUZZ_STREAM_REPS", 1))))
+@pytest.mark.parametrize("nstates", [2, 1])
+def test_decompress_many_random(torch_cuda, nstates, rep):
+    """fse_decompress2_many / fse_decompress_many (host buffers, the batching
+    drop-in) on the same random stream sets as test_decompress_streams:
+    every stream's bytes or status equal the oracle's single-stream call."""
+    _streams_case(nstates, 0x3A11 + nstates + 2 * rep + int(os.environ.get("FSEHIP_FUZZ_SEED", 0)), draw=2,
+                  host=True)
+
+
+def _streams_case(nstates, seed, draw, host=False):
     """60 crate streams of one seed.  draw 1: the lists of the sweep that found
     the regressions above; draw 2 adds table logs 5..8, 14, 15, longer streams
-    and other strides."""
-    from entropy_coders_amd import decompress_streams
+    and other strides.  host: through fse_decompress2_many (any table log in
+    one call) instead of fsehip_decompress_streams at each bound."""
+    from entropy_coders_amd import decompress2_many, decompress_streams
 
     rng = np.random.default_rng(seed)
     stride = 24000 if draw == 1 else int(rng.choice([24000, 40016, 65536]))
@@ -207,6 +218,16 @@ def _streams_case(nstates, seed, draw):
         streams.append(bytes(comp))
         logs.append((comp[0] & 15) + 5)
     ref_dec = O.decompress2 if nstates == 2 else O.decompress
+    if host:
+        got = decompress2_many(streams, stride, nstates=nstates)
+        for i, (x, g) in enumerate(zip(streams, got)):
+            try:
+                want = ref_dec(x, stride)
+            except O.OracleError as e:
+                assert g == e.code, (i, e.code, g)
+                continue
+            assert g == want, i
+        return
     for mtl in (11, 12, 13, 14, 15):
         got = decompress_streams(streams, stride, nstates=nstates, max_table_log=mtl)
         for i, (x, g) in enumerate(zip(streams, got)):
