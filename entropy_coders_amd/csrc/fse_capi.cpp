@@ -881,53 +881,38 @@ static void for_streams(size_t n, uint64_t bytes, Fn fn) {
 }
 }  // extern "C++"
 
-static int decompress_many(const uint8_t* const* srcs, const size_t* src_lens, size_t n_streams, uint8_t* dst,
-                           size_t dst_stride, size_t* dst_lens, int32_t* statuses, uint32_t nstates) {
-    if (n_streams == 0) return FSE_OK;
-    if (!srcs || !src_lens || !dst || !dst_lens || !statuses || dst_stride == 0) return FSE_ERR_BAD_ARG;
-    if (n_streams > (1u << 24) || dst_stride > 0x7FFFFFFFull) return FSE_ERR_UNSUPPORTED;
-    if (!device_ok()) return FSE_ERR_NO_DEVICE;
-    if (n_streams <= 2) {
-        for (size_t i = 0; i < n_streams; ++i) {
-            size_t len = 0;
-            statuses[i] = decompress_one(srcs[i], src_lens[i], dst + i * dst_stride, dst_stride, &len, nstates);
-            if (statuses[i] == FSE_ERR_HIP || statuses[i] == FSE_ERR_NO_DEVICE) return statuses[i];
-            dst_lens[i] = statuses[i] == FSE_OK ? len : 0;
-        }
-        return FSE_OK;
-    }
-    // per-stream statuses the reference's own checks give before any decode
+// One batch: the streams idx[0..m) (each 0 < n <= kManyStream, non-null),
+// staged at a common stride, decoded as fsehip_decompress_streams does.
+static int decompress_batch(const uint8_t* const* srcs, const size_t* src_lens, const std::vector<size_t>& idx,
+                            uint8_t* dst, size_t dst_stride, size_t* dst_lens, int32_t* statuses, uint32_t nstates) {
+    const size_t m = idx.size();
     size_t maxn = 1;
     uint32_t lmax = 11;
-    for (size_t i = 0; i < n_streams; ++i) {
-        const size_t n = src_lens[i];
-        if (n == 0 || n > kMaxBlock || !srcs[i]) continue;
-        maxn = std::max(maxn, n);
+    uint64_t in_total = 0;
+    for (size_t i : idx) {
+        maxn = std::max(maxn, src_lens[i]);
+        in_total += src_lens[i];
         lmax = std::max<uint32_t>(lmax, (uint32_t)(srcs[i][0] & 15u) + LOG_MIN_HOST);  // histogram.rs:438
     }
     const uint32_t mtl = lmax <= 11u ? 11u : lmax <= 12u ? 12u : 15u;
     const uint64_t in_stride = round_up(maxn + 32, 256);
     const uint64_t out_stride = round_up(dst_stride, 16);
-    const uint64_t head = round_up(4ull * n_streams, 256);  // the lengths ahead of the streams
-    const uint64_t in_bytes = head + in_stride * n_streams;
-    const uint64_t rec = round_up(8ull * n_streams, 256);  // (length, status) per stream ahead of the output
-    const uint64_t out_bytes = rec + out_stride * n_streams;
+    const uint64_t head = round_up(4ull * m, 256);  // the lengths ahead of the streams
+    const uint64_t in_bytes = head + in_stride * m;
+    const uint64_t rec = round_up(8ull * m, 256);  // (length, status) per stream ahead of the output
+    const uint64_t out_bytes = rec + out_stride * m;
     uint8_t* d_in = g_stage.get(4, in_bytes);
     uint8_t* d_out = g_stage.get(5, out_bytes);
     uint8_t* h_in = g_pin.get(0, in_bytes);
     uint8_t* h_out = g_pin.get(1, out_bytes);
     if (!d_in || !d_out || !h_in || !h_out) return FSE_ERR_HIP;
     uint32_t* lens = reinterpret_cast<uint32_t*>(h_in);
-    uint64_t in_total = 0;
-    for (size_t i = 0; i < n_streams; ++i) in_total += src_lens[i] <= kMaxBlock ? src_lens[i] : 0;
-    for_streams(n_streams, in_total, [&](size_t i) {
-        const size_t n = src_lens[i];
-        const bool ok = n != 0 && n <= kMaxBlock && srcs[i];
-        uint8_t* s = h_in + head + i * in_stride;
-        lens[i] = ok ? (uint32_t)n : 0u;
-        if (ok) memcpy(s, srcs[i], n);
-        const size_t z = ok ? n : 0;
-        memset(s + z, 0, std::min<uint64_t>(in_stride, round_up(z, 32) + 32) - z);
+    for_streams(m, in_total, [&](size_t k) {
+        const size_t n = src_lens[idx[k]];
+        uint8_t* s = h_in + head + k * in_stride;
+        lens[k] = (uint32_t)n;
+        memcpy(s, srcs[idx[k]], n);
+        memset(s + n, 0, std::min<uint64_t>(in_stride, round_up(n, 32) + 32) - n);
     });
     auto fail = [](int rc) {  // nothing may still read or write the pinned buffers
         (void)hipStreamSynchronize(nullptr);
@@ -936,9 +921,9 @@ static int decompress_many(const uint8_t* const* srcs, const size_t* src_lens, s
     if (hipMemcpyAsync(d_in, h_in, in_bytes, hipMemcpyHostToDevice, nullptr) != hipSuccess) return fail(FSE_ERR_HIP);
     const uint32_t* d_len = reinterpret_cast<const uint32_t*>(d_in);
     uint32_t* d_olen = reinterpret_cast<uint32_t*>(d_out);
-    int32_t* d_stat = reinterpret_cast<int32_t*>(d_out + 4ull * n_streams);
+    int32_t* d_stat = reinterpret_cast<int32_t*>(d_out + 4ull * m);
     const fsehip_params p{(uint32_t)out_stride, 0, 0, mtl, nstates};
-    int rc = with_dtables_n(&p, d_in + head, in_stride, d_len, n_streams, nullptr,
+    int rc = with_dtables_n(&p, d_in + head, in_stride, d_len, m, nullptr,
                             [&](const uint32_t* dt, const int32_t* info, Lease& lease) {
                                 fsehip::DecParams P{};
                                 P.nstates = nstates;
@@ -948,7 +933,7 @@ static int decompress_many(const uint8_t* const* srcs, const size_t* src_lens, s
                                 P.out = d_out + rec;
                                 P.n_total = 0;  // reference mode: each stream ends where the crate stops
                                 P.block_size = (uint32_t)out_stride;
-                                P.n_blocks = (uint32_t)n_streams;
+                                P.n_blocks = (uint32_t)m;
                                 P.out_cap = (uint32_t)dst_stride;
                                 P.status = d_stat;
                                 P.out_len = d_olen;
@@ -963,19 +948,70 @@ static int decompress_many(const uint8_t* const* srcs, const size_t* src_lens, s
     if (hipMemcpyAsync(h_out, d_out, out_bytes, hipMemcpyDeviceToHost, nullptr) != hipSuccess) return fail(FSE_ERR_HIP);
     if (hipStreamSynchronize(nullptr) != hipSuccess) return FSE_ERR_HIP;
     const uint32_t* olen = reinterpret_cast<const uint32_t*>(h_out);
-    const int32_t* ost = reinterpret_cast<const int32_t*>(h_out + 4ull * n_streams);
+    const int32_t* ost = reinterpret_cast<const int32_t*>(h_out + 4ull * m);
     uint64_t out_total = 0;
-    for (size_t i = 0; i < n_streams; ++i) out_total += ost[i] == FSE_OK ? olen[i] : 0;
-    for_streams(n_streams, out_total, [&](size_t i) {
-        const size_t n = src_lens[i];
-        int32_t st = ost[i];
-        if (n == 0) st = FSE_ERR_EMPTY;  // BitStreamReader::new asserts (stream_reader.rs:17)
-        else if (!srcs[i]) st = FSE_ERR_BAD_ARG;
-        else if (n > kMaxBlock) st = FSE_ERR_UNSUPPORTED;
-        statuses[i] = st;
-        dst_lens[i] = st == FSE_OK ? olen[i] : 0;
-        if (st == FSE_OK) memcpy(dst + i * dst_stride, h_out + rec + i * out_stride, olen[i]);
+    for (size_t k = 0; k < m; ++k) out_total += ost[k] == FSE_OK ? olen[k] : 0;
+    for_streams(m, out_total, [&](size_t k) {
+        const size_t i = idx[k];
+        statuses[i] = ost[k];
+        dst_lens[i] = ost[k] == FSE_OK ? olen[k] : 0;
+        if (ost[k] == FSE_OK) memcpy(dst + i * dst_stride, h_out + rec + k * out_stride, olen[k]);
     });
+    return FSE_OK;
+}
+
+// Many host streams in one call (lib.rs:187-248 per stream).  Streams the
+// batch takes (up to 4 MiB each) go in groups of at most kManyStage bytes
+// of staging each way; longer ones, and calls of one or two streams, take
+// the single-stream path one by one (its chain is ~2x faster than a serial
+// ring chain, and a lone long stream should not set the stride of all).
+constexpr size_t kManyStream = size_t(4) << 20;
+constexpr uint64_t kManyStage = uint64_t(512) << 20;
+static int decompress_many(const uint8_t* const* srcs, const size_t* src_lens, size_t n_streams, uint8_t* dst,
+                           size_t dst_stride, size_t* dst_lens, int32_t* statuses, uint32_t nstates) {
+    if (n_streams == 0) return FSE_OK;
+    if (!srcs || !src_lens || !dst || !dst_lens || !statuses || dst_stride == 0) return FSE_ERR_BAD_ARG;
+    if (n_streams > (1u << 24) || dst_stride > 0x7FFFFFFFull) return FSE_ERR_UNSUPPORTED;
+    if (!device_ok()) return FSE_ERR_NO_DEVICE;
+    const uint64_t out_stride = round_up(dst_stride, 16);
+    std::vector<size_t> single, group;
+    auto run_group = [&]() -> int {
+        if (group.empty()) return FSE_OK;
+        if (group.size() <= 2) {  // not worth the batch kernels' fixed cost
+            single.insert(single.end(), group.begin(), group.end());
+            group.clear();
+            return FSE_OK;
+        }
+        const int rc = decompress_batch(srcs, src_lens, group, dst, dst_stride, dst_lens, statuses, nstates);
+        group.clear();
+        return rc;
+    };
+    uint64_t gmax = 0;  // the group's largest staged stream
+    for (size_t i = 0; i < n_streams; ++i) {
+        const size_t n = src_lens[i];
+        if (n == 0 || !srcs[i] || n > kManyStream || n_streams <= 2 || out_stride > kManyStage / 4) {
+            single.push_back(i);  // statuses and long streams: the single call's own path
+            continue;
+        }
+        const uint64_t in_s = round_up(n + 32, 256), g = std::max(gmax, in_s);
+        if (!group.empty() && (group.size() + 1) * std::max(g, out_stride) > kManyStage) {
+            if (int rc = run_group()) return rc;
+            gmax = 0;
+        }
+        group.push_back(i);
+        gmax = std::max(gmax, in_s);
+    }
+    if (int rc = run_group()) return rc;
+    for (size_t i : single) {
+        size_t len = 0;
+        const int32_t st = src_lens[i] == 0 ? FSE_ERR_EMPTY  // BitStreamReader::new asserts (stream_reader.rs:17)
+                           : !srcs[i]      ? FSE_ERR_BAD_ARG
+                                           : decompress_one(srcs[i], src_lens[i], dst + i * dst_stride, dst_stride,
+                                                            &len, nstates);
+        if (st == FSE_ERR_HIP || st == FSE_ERR_NO_DEVICE) return st;
+        statuses[i] = st;
+        dst_lens[i] = st == FSE_OK ? len : 0;
+    }
     return FSE_OK;
 }
 

@@ -81,8 +81,11 @@ int fse_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, s
  * dst + i * dst_stride with at most dst_stride bytes; dst_lens[i] = bytes
  * decoded and statuses[i] = its status, as the single call would return it
  * (EMPTY, BAD_HEADER, NO_MARKER, TOO_SHORT, SINGLE_SYMBOL, DST_TOO_SMALL,
- * UNSUPPORTED above 2^28 bytes).  Returns FSE_OK when the batch ran (look at
- * statuses), or a call-level error (BAD_ARG, NO_DEVICE, HIP).
+ * UNSUPPORTED above 2^28 bytes; a null srcs[i] with src_lens[i] > 0 is
+ * BAD_ARG).  Returns FSE_OK when the batch ran (look at statuses), or a
+ * call-level error (BAD_ARG, NO_DEVICE, HIP).  Streams up to 4 MiB are
+ * batched, in groups of at most 512 MiB of staging each way; longer ones
+ * (and dst_stride above 128 MiB) take the single-stream path one by one.
  *
  * Where the GPU pays.  A lone stream is one serial chain: fse_decompress2
  * takes ~1.4 ms per 64 KiB call on MI355X against ~0.14-0.4 ms on one host

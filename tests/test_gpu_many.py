@@ -95,3 +95,21 @@ def test_many_streams_short_stride_and_small_batches(torch_cuda):
         assert got == [s.tobytes() for s in srcs[:k]]
     assert decompress2_many([], 16) == []
     assert decompress2(comps[0]) == srcs[0].tobytes()
+
+
+def test_many_streams_mixed_sizes_and_groups(torch_cuda):
+    """Streams above the batch's 4 MiB take the single-stream path inside the
+    same call, and a stride large enough to split the batch into several
+    staging groups gives the same per-stream results."""
+    from entropy_coders_amd import decompress2_many
+
+    big = O.generate(2, 0.0, 0x5EED0009, 0, (5 << 20) + 333)  # near-uniform: > 4 MiB compressed
+    smalls = [O.generate(0, 0.155, 0x5EED0002, i, 65536) for i in range(6)]
+    comps = [O.compress2(s)[0] for s in smalls[:3]] + [O.compress2(big)[0]] + [O.compress2(s)[0] for s in smalls[3:]]
+    assert len(comps[3]) > 4 << 20
+    got = decompress2_many(comps, 6 << 20)
+    want = [s.tobytes() for s in smalls[:3]] + [big.tobytes()] + [s.tobytes() for s in smalls[3:]]
+    assert got == want
+    # 96 MiB strides: 5 streams per 512 MiB staging group -> two groups
+    got = decompress2_many([O.compress2(s)[0] for s in smalls] * 2, 96 << 20)
+    assert got == [s.tobytes() for s in smalls] * 2
