@@ -42,6 +42,9 @@ __device__ __forceinline__ uint4 load_chunk(const uint8_t* blk, uint32_t n, uint
 #ifndef FSEHIP_ENC_ABL
 #define FSEHIP_ENC_ABL 0  // encoder timing probes (variant builds only)
 #endif
+#ifndef FSEHIP_ENC_PF
+#define FSEHIP_ENC_PF 4  // source chunk registers of the emit pass (PF - 1 loads in flight)
+#endif
 struct EncTab {
     const uint2* tt;  // {deltaNbBits, LDS address of stateTable + 2 * deltaFindState}
 };
@@ -366,7 +369,11 @@ __device__ __forceinline__ EncState enc_range(const uint8_t* __restrict__ blk, u
     }
     if (c_hi < c_lo || (RP && tr.done)) return EncState{x0, x1, bits};
     auto ld = [&](int32_t c) { return v[c < c_lo ? c_lo : c]; };
-    uint4 q0 = ld(c_hi), q1 = ld(c_hi - 1), q2 = ld(c_hi - 2), q3 = ld(c_hi - 3);
+    // source chunks in flight: PF - 1 ahead of the one being encoded
+    constexpr int PF = emits<MODE>() ? FSEHIP_ENC_PF : 4;
+    uint4 q[PF];
+#pragma unroll
+    for (int k = 0; k < PF; ++k) q[k] = ld(c_hi - k);
     auto body = [&](const uint4& q, int32_t c) {
         enc_chunk<MODE, true, NS>(q, (uint32_t)c << CS, pb, x0, x1, T, bits, em);
         if (emits<MODE>()) em.drain();
@@ -375,19 +382,18 @@ __device__ __forceinline__ EncState enc_range(const uint8_t* __restrict__ blk, u
         if (TRACK) track();
     };
     auto stop = [&](int32_t cn) { return cn < c_lo || (RP && tr.done); };
-    for (int32_t c = c_hi;; c -= 4) {
-        body(q0, c);
-        if (stop(c - 1)) break;
-        q0 = ld(c - 4);
-        body(q1, c - 1);
-        if (stop(c - 2)) break;
-        q1 = ld(c - 5);
-        body(q2, c - 2);
-        if (stop(c - 3)) break;
-        q2 = ld(c - 6);
-        body(q3, c - 3);
-        if (stop(c - 4)) break;
-        q3 = ld(c - 7);
+    for (int32_t c = c_hi;; c -= PF) {
+        bool done = false;
+#pragma unroll
+        for (int k = 0; k < PF; ++k) {
+            body(q[k], c - k);
+            if (stop(c - k - 1)) {
+                done = true;
+                break;
+            }
+            q[k] = ld(c - k - PF);
+        }
+        if (done) break;
     }
     return EncState{x0, x1, bits};
 }
