@@ -58,33 +58,37 @@ __device__ __forceinline__ uint32_t lds_addr_of(P* p) {
     return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) P*)p;
 }
 
-// Bit emitter into a 32-bit-word view of the output slot.  Bits are
-// appended LSB-first (writer.rs:140-180); every completed word is stored,
-// including the lane's first word, whose low bits belong to the previous
-// lane: the merge step later rewrites each boundary word with the OR of both
-// lanes' bits.
 // Bit writer of one lane's range: BitStackWriter order (writer.rs:140-222),
-// words through a 16-word LDS ring (RING_STRIDE words per lane: 16-byte
-// aligned, conflict-free dwordx4 reads).  Every 8-word group of the slot
-// that lies wholly inside the lane's range leaves as one 32-byte store (two
-// dwordx4; L2 merges a lane's consecutive groups into whole lines) once the
-// lane has moved past it; the partial groups at either end leave as dword
-// stores.  (A 32-word ring with 64-byte groups needed 9 KiB of LDS per
-// workgroup, which held the encoder at 8 workgroups per CU.)  The lane's first word, when
-// it shares it with the lane above (off % 32 != 0), is never stored: its
-// value (head_val) goes to the merge list, like the lane's last partial
-// word.  Stores stay below wlim (the slot's words).
+// LSB-first words through a 24-word LDS ring.  Every 16-word (64-byte)
+// group of the slot that lies wholly inside the lane's range leaves as four
+// dwordx4 stores once the lane has moved past it: whole aligned 64-byte
+// pieces.  (32-byte groups, the round-4 layout, left 64-byte pieces half
+// written at a time; as whole pieces the same bytes cost 0.05 ms less per
+// GiB, profiles/r05/enc_store/.)  The partial groups at either end of the
+// lane leave as dword stores.  The lane's first word, when it shares it with
+// the lane above (off % 32 != 0), is never stored: its value (head_val)
+// goes to the merge list, like the lane's last partial word, and the merge
+// step rewrites each boundary word with the OR of both lanes' bits.  Stores
+// stay below wlim (the slot's words).
+//
+// The ring: a group is stored at the first drain after it completes, and
+// drain runs every <= 8 pairs (<= 8 new words even at L = 15), so the ring
+// holds the pending group's 16 words plus <= 8 more: 24 slots, word w at
+// slot w mod 24 (a group's four 4-word pieces are 4-aligned slots, since
+// 16 g mod 24 is a multiple of 8).
+constexpr uint32_t RING_WORDS = 24;
 struct Emit {
     uint32_t lo, hi;    // pending bits: lo = the word being filled, hi = bits past it
     uint32_t nacc;
     uint32_t word;      // index of the word being filled
+    uint32_t rix;       // its ring slot, word mod RING_WORDS
     uint32_t w0;        // first word index of the lane
     uint32_t head_val;  // lane's bits of word w0 (valid once word > w0 and the head group left)
     uint32_t wlim;      // words in the slot: stores never leave it
-    uint32_t gs;        // next 8-word group to store
+    uint32_t gs;        // next 16-word group to store
     bool skip_head;
     uint32_t* gw;
-    uint32_t* ring;     // LDS, 16 words, 16-byte aligned
+    uint32_t* ring;     // LDS, RING_WORDS words, 16-byte aligned
     __device__ __forceinline__ void start(uint32_t* g, uint32_t off, uint32_t lim = 0xFFFFFFFFu,
                                           uint32_t* r = nullptr) {
         gw = g;
@@ -93,8 +97,9 @@ struct Emit {
         lo = hi = 0;
         nacc = off & 31u;
         word = off >> 5;
+        rix = word % RING_WORDS;
         w0 = word;
-        gs = word >> 3;
+        gs = word >> 4;
         skip_head = (off & 31u) != 0u;
         head_val = 0;
     }
@@ -106,42 +111,60 @@ struct Emit {
     }
     // The ring slot of the word being filled is written every time: until
     // the word completes nothing reads it, so no branch is needed.  Callers
-    // flush before nacc can reach 64 (<= 2 x 12 bits per flush).
+    // flush before nacc can reach 64 (<= 2 x 15 bits per flush).
     __device__ __forceinline__ void flush() {
         const bool f = nacc >= 32u;
-        ring[word & 15u] = lo;
+        ring[rix] = lo;
         lo = f ? hi : lo;
         hi = 0;  // nacc < 32 after the flush
         nacc &= 31u;
         word += f ? 1u : 0u;
+        rix += f ? 1u : 0u;
+        rix = rix == RING_WORDS ? 0u : rix;
     }
     __device__ __forceinline__ uint32_t pos() const { return word * 32u + nacc; }
+    // Words [a, b) of the lane's range, within one group: dwords up to the
+    // next 4-word boundary, whole 4-word pieces as dwordx4, dwords after
+    // (pieces never straddle the ring's end: its slots are 4-aligned)
     __device__ __forceinline__ void store_words(uint32_t a, uint32_t b) {
-        for (uint32_t i = a; i < b; ++i)
-            if (i < wlim) gw[i] = ring[i & 15u];
+        b = min(b, wlim);
+        uint32_t i = a;
+        for (; i < b && (i & 3u); ++i) gw[i] = ring[i % RING_WORDS];
+        for (; i + 4u <= b; i += 4u)
+            *reinterpret_cast<uint4*>(gw + i) = *reinterpret_cast<const uint4*>(ring + i % RING_WORDS);
+        for (; i < b; ++i) gw[i] = ring[i % RING_WORDS];
     }
     __device__ __forceinline__ void store_group(uint32_t g) {
-        const uint32_t base = g << 3;
-        if (g == (w0 >> 3) && ((w0 & 7u) != 0u || skip_head)) {  // the lane's first group: its own words only
-            if (skip_head) head_val = ring[w0 & 15u];
-            store_words(skip_head ? w0 + 1u : w0, base + 8u);
-        } else if (base + 8u <= wlim) {
-            const uint4* r = reinterpret_cast<const uint4*>(ring + (base & 15u));
+        const uint32_t base = g << 4;
+        if (g == (w0 >> 4) && ((w0 & 15u) != 0u || skip_head)) {  // the lane's first group: its own words only
+            if (skip_head) head_val = ring[w0 % RING_WORDS];
+            store_words(skip_head ? w0 + 1u : w0, base + 16u);
+        } else if (base + 16u <= wlim) {
+            const uint32_t r0 = base % RING_WORDS;
 #if FSEHIP_ENC_ABL & 1  // probe (timing only, wrong output): the same stores into the slot's first 2 KiB (L2-resident lines)
             uint4* o = reinterpret_cast<uint4*>(gw + (base & 511u));
 #else
             uint4* o = reinterpret_cast<uint4*>(gw + base);
 #endif
-            const uint4 a = r[0], b = r[1];
-            o[0] = a;
-            o[1] = b;
+#pragma unroll
+            for (uint32_t q = 0; q < 4; ++q) {
+                uint32_t rq = r0 + 4u * q;
+                rq = rq >= RING_WORDS ? rq - RING_WORDS : rq;
+                const uint4 a = *reinterpret_cast<const uint4*>(ring + rq);
+#if FSEHIP_ENC_ABL & 8  // probe (timing only, wrong output): the group's ring reads without its stores
+                asm volatile("; sink %0 %1 %2 %3" ::"v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w));
+                (void)o;
+#else
+                o[q] = a;
+#endif
+            }
         }
     }
     // Store the group the lane has moved past, if any (called every <= 8
-    // pairs: <= 6 new words, fewer than a group, so the ring never overruns
+    // pairs: <= 8 new words, fewer than a group, so the ring never overruns
     // a pending group and at most one group completes between calls).
     __device__ __forceinline__ void drain() {
-        if (word >= (gs + 1u) << 3) {
+        if (word >= (gs + 1u) << 4) {
             store_group(gs);
             ++gs;
         }
@@ -149,25 +172,24 @@ struct Emit {
     // End of the lane: remaining whole groups, then the whole words of the
     // last group (the partial word stays in acc for the merge list).
     __device__ __forceinline__ void finish() {
-        while (word >= (gs + 1u) << 3) {
+        while (word >= (gs + 1u) << 4) {
             store_group(gs);
             ++gs;
         }
-        uint32_t lo = gs << 3;
-        if (gs == (w0 >> 3)) {
+        uint32_t lo = gs << 4;
+        if (gs == (w0 >> 4)) {
             lo = w0;
             if (skip_head) {
                 lo = w0 + 1u;
-                if (word > w0) head_val = ring[w0 & 15u];
+                if (word > w0) head_val = ring[w0 % RING_WORDS];
             }
         }
         store_words(lo, word);
     }
 };
 
-// Words per lane of the emit ring in LDS: 16 used; the stride of 20 puts
-// the 16 lanes of each dwordx4 read group on distinct 16-byte bank slots.
-constexpr uint32_t RING_STRIDE = 20;
+// Words per lane of the emit ring in LDS (16-byte aligned rows).
+constexpr uint32_t RING_STRIDE = RING_WORDS;
 
 // A lane's checkpoints (its range holds at most S / interval of them) are
 // kept in registers and written together after its emit pass: recorded one
@@ -469,14 +491,19 @@ struct EncSmem {
             uint16_t cumul[256];
             uint32_t cnt[256];
         } p1;
-        struct {
-            union {
+        // phase 2, three lifetimes over the same bytes: the count / repair
+        // rounds (trajectories, end states), the emit pass (its ring), and
+        // the boundary-word merge after it
+        union {
+            struct {
                 uint2 cp[64 * TRACK_SLOTS];  // count-pass trajectories (Track)
-                uint32_t ring[64 * RING_STRIDE];  // emit: 16-word output ring per lane (Emit)
+                uint32_t cntF[BPW][T + 1];   // each lane's end state
             } u;
-            uint32_t cntF[BPW][T + 1];
-            uint32_t mword[BPW][2 * (T + 1)];
-            uint32_t mval[BPW][2 * (T + 1)];
+            __attribute__((aligned(16))) uint32_t ring[64 * RING_STRIDE];  // emit: output ring per lane (Emit)
+            struct {
+                uint32_t mword[BPW][2 * (T + 1)];
+                uint32_t mval[BPW][2 * (T + 1)];
+            } mg;
         } p2;
     } ph;
 #if FSEHIP_ENC_ABL & 2
@@ -654,7 +681,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
             EncState e0 = (k == ktop) ? top_start<PASS_COUNT, NS>(blk, n, tab, em) : EncState{start & 0xFFFFu, start >> 16, 0u};
             e0 = enc_range<MC, NS>(blk, n, pa, pb, e0, tab, em, ck, tr);
             bits = e0.bits;
-            sm.ph.p2.cntF[b][k] = e0.x0 | (e0.x1 << 16);
+            sm.ph.p2.u.cntF[b][k] = e0.x0 | (e0.x1 << 16);
             track_fixup(tr, nslot, -1, bits);
         }
         FSE_STAMP(P, 5);
@@ -664,7 +691,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
             bool bad = false;
             uint32_t nbF = 0;
             if (act && k < ktop) {
-                nbF = sm.ph.p2.cntF[b][k + 1];
+                nbF = sm.ph.p2.u.cntF[b][k + 1];
                 bad = nbF != start;
             }
             __syncthreads();
@@ -680,7 +707,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
                 const EncState e0 = enc_range<MR, NS>(blk, n, pa, pb, EncState{start & 0xFFFFu, start >> 16, 0u},
                                                            tab, em, ck, tr);
                 bits = e0.bits;
-                if (!tr.done) sm.ph.p2.cntF[b][k] = e0.x0 | (e0.x1 << 16);  // did not converge: new end state
+                if (!tr.done) sm.ph.p2.u.cntF[b][k] = e0.x0 | (e0.x1 << 16);  // did not converge: new end state
                 track_fixup(tr, nslot, tr.done ? (int32_t)tr.jstar : -1, bits);
             }
         }
@@ -705,14 +732,12 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     const bool fits = (uint64_t)total_bits <= P.slot_bytes * 8ull && !(P.debug & 2u) && !(FSEHIP_ENC_ABL & 2);
     uint32_t* gw = reinterpret_cast<uint32_t*>(P.out + gb * P.slot_bytes);
 
-    // emit pass
-    for (uint32_t e = k; e < 2u * (T + 1u); e += T) {
-        if (b < BPW) sm.ph.p2.mword[b][e] = 0xFFFFFFFFu;
-    }
+    // emit pass (its ring overlays the trajectories and end states: every
+    // lane is past the repair rounds here)
     __syncthreads();
     if (act && fits) {
         em.start(gw, off, (P.debug & 4u) ? 0u : (uint32_t)(P.slot_bytes >> 2),  // debug bit 2: no payload stores (ablation)
-                 &sm.ph.p2.u.ring[lane * RING_STRIDE]);
+                 &sm.ph.p2.ring[lane * RING_STRIDE]);
         {
             if (P.sidecar && P.ckpt_interval) {
                 ck.base = P.sidecar + gb * P.ckpt_per_block;
@@ -745,21 +770,29 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
             }
         }
         em.finish();
-        // boundary words -> merge list (entry order = stream order)
+    }
+    // boundary words -> merge list (entry order = stream order); the list
+    // overlays the ring, so every lane's ring reads are done first
+    __syncthreads();
+    for (uint32_t e = k; e < 2u * (T + 1u); e += T) {
+        if (b < BPW) sm.ph.p2.mg.mword[b][e] = 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    if (act && fits) {
         const uint32_t slot = 2u * (T - k);
         if ((off & 31u) != 0u && em.word > em.w0) {  // first word stored with the low bits empty
-            sm.ph.p2.mword[b][slot] = em.w0;
-            sm.ph.p2.mval[b][slot] = em.head_val;
+            sm.ph.p2.mg.mword[b][slot] = em.w0;
+            sm.ph.p2.mg.mval[b][slot] = em.head_val;
         }
         if (em.nacc) {  // last word never stored
-            sm.ph.p2.mword[b][slot + 1] = em.word;
-            sm.ph.p2.mval[b][slot + 1] = em.lo;
+            sm.ph.p2.mg.mword[b][slot + 1] = em.word;
+            sm.ph.p2.mg.mval[b][slot + 1] = em.lo;
         }
     }
     // header: whole words were stored in phase 1; the last partial word is merged
     if (live && fits && k == 0 && (hl & 3u)) {
-        sm.ph.p2.mword[b][0] = hl / 4u;
-        sm.ph.p2.mval[b][0] = sm.info_hv[b];
+        sm.ph.p2.mg.mword[b][0] = hl / 4u;
+        sm.ph.p2.mg.mval[b][0] = sm.info_hv[b];
     }
     FSE_STAMP(P, 7);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stores above land before the merge rewrites
@@ -768,22 +801,22 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     if (live && fits) {
         constexpr uint32_t NE = 2u * (T + 1u);
         for (uint32_t e = k; e < NE; e += T) {
-            const uint32_t w = sm.ph.p2.mword[b][e];
+            const uint32_t w = sm.ph.p2.mg.mword[b][e];
             if (w == 0xFFFFFFFFu) continue;
             bool first = true;
             for (int q = (int)e - 1; q >= 0; --q) {
-                const uint32_t wq = sm.ph.p2.mword[b][q];
+                const uint32_t wq = sm.ph.p2.mg.mword[b][q];
                 if (wq == 0xFFFFFFFFu) continue;
                 first = (wq != w);
                 break;
             }
             if (!first) continue;
-            uint32_t v = sm.ph.p2.mval[b][e];
+            uint32_t v = sm.ph.p2.mg.mval[b][e];
             for (uint32_t q = e + 1; q < NE; ++q) {
-                const uint32_t wq = sm.ph.p2.mword[b][q];
+                const uint32_t wq = sm.ph.p2.mg.mword[b][q];
                 if (wq == 0xFFFFFFFFu) continue;
                 if (wq != w) break;
-                v |= sm.ph.p2.mval[b][q];
+                v |= sm.ph.p2.mg.mval[b][q];
             }
             if (w < (uint32_t)(P.slot_bytes >> 2)) gw[w] = v;
         }
