@@ -154,6 +154,8 @@ struct Emit {
 #if FSEHIP_ENC_ABL & 8  // probe (timing only, wrong output): the group's ring reads without its stores
                 asm volatile("; sink %0 %1 %2 %3" ::"v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w));
                 (void)o;
+#elif FSEHIP_ENC_ABL & 16  // A/B (timing only): non-temporal group stores
+                __builtin_nontemporal_store(u32x4{a.x, a.y, a.z, a.w}, reinterpret_cast<u32x4*>(o + q));
 #else
                 o[q] = a;
 #endif
