@@ -76,7 +76,10 @@ __device__ __forceinline__ uint32_t lds_addr_of(P* p) {
 // holds the pending group's 16 words plus <= 8 more: 24 slots, word w at
 // slot w mod 24 (a group's four 4-word pieces are 4-aligned slots, since
 // 16 g mod 24 is a multiple of 8).
-constexpr uint32_t RING_WORDS = 24;
+#ifndef FSEHIP_ENC_RING
+#define FSEHIP_ENC_RING 24  // emit ring words per lane (A/B builds: 32)
+#endif
+constexpr uint32_t RING_WORDS = FSEHIP_ENC_RING;
 struct Emit {
     uint32_t lo, hi;    // pending bits: lo = the word being filled, hi = bits past it
     uint32_t nacc;
@@ -120,7 +123,8 @@ struct Emit {
         nacc &= 31u;
         word += f ? 1u : 0u;
         rix += f ? 1u : 0u;
-        rix = rix == RING_WORDS ? 0u : rix;
+        if constexpr ((RING_WORDS & (RING_WORDS - 1u)) == 0u) rix &= RING_WORDS - 1u;
+        else rix = rix == RING_WORDS ? 0u : rix;
     }
     __device__ __forceinline__ uint32_t pos() const { return word * 32u + nacc; }
     // Words [a, b) of the lane's range, within one group: dwords up to the
