@@ -49,8 +49,14 @@ struct EncTab {
     const uint2* tt;  // {deltaNbBits, LDS address of stateTable + 2 * deltaFindState}
 };
 typedef __attribute__((address_space(3))) const uint16_t lds_cu16;
+typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
 __device__ __forceinline__ uint32_t st_at(uint32_t lds_addr) {
+#if FSEHIP_ENC_ABL & 32  // A/B: the entry's dword read whole (ds_read_b32) and its half extracted
+    const uint32_t v = *(lds_cu32*)(uintptr_t)(lds_addr & ~3u);
+    return __builtin_amdgcn_ubfe(v, (lds_addr & 2u) << 3, 16u);
+#else
     return *(lds_cu16*)(uintptr_t)lds_addr;
+#endif
 }
 // LDS byte address of a __shared__ object
 template <class P>
@@ -255,12 +261,41 @@ struct EncState {
     uint32_t x0, x1, bits;
 };
 
+// One state step on the dependent chain x -> stateTable[(x >> nb) + dFS],
+// nb = (deltaNbBits + x) >> 16: updates x and returns the sum deltaNbBits + x,
+// whose upper word is nb.  FSEHIP_ENC_SDWA: the shift takes nb as the sum's
+// upper word (SDWA src0_sel:WORD_1), so no VALU op computes nb on the chain
+// (add, shift, shift-add, ds_read_u16); callers take nb = sum >> 16 (or add
+// sums as packed halves, FSEHIP_ENC_PKB) off the chain.
+#ifndef FSEHIP_ENC_SDWA
+#define FSEHIP_ENC_SDWA 0
+#endif
+#ifndef FSEHIP_ENC_PKB
+#define FSEHIP_ENC_PKB 0
+#endif
+__device__ __forceinline__ uint32_t state_step(uint32_t& x, const uint2 t) {
+    const uint32_t sum = t.x + x;
+#if FSEHIP_ENC_SDWA
+    uint32_t y;
+    asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD"
+        : "=v"(y)
+        : "v"(sum), "v"(x));
+    x = st_at((y << 1) + t.y);
+#else
+    x = st_at(((x >> (sum >> 16)) << 1) + t.y);
+#endif
+    return sum;
+}
+// Packed 16-bit add (v_pk_add_u16): the upper halves add without a carry in
+// from the lower ones, so adding step sums accumulates their nb.
+typedef uint16_t u16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_add16(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2_t, a) + __builtin_bit_cast(u16x2_t, b));
+}
+
 // Encoder::encode_raw (fse.rs:227-239): returns nb, updates x.
 __device__ __forceinline__ uint32_t enc_step(uint32_t& x, uint32_t s, const EncTab& T) {
-    const uint2 t = T.tt[s];
-    const uint32_t nb = (t.x + x) >> 16;
-    x = st_at(((x >> nb) << 1) + t.y);
-    return nb;
+    return state_step(x, T.tt[s]) >> 16;
 }
 
 // One 16-byte chunk.  NS = 2 (fse_compress2): pairs c8+7 .. c8 (lib.rs:167-176:
@@ -271,6 +306,9 @@ template <int MODE, bool FULL, int NS>
 __device__ __forceinline__ void enc_chunk(const uint4& q, uint32_t c8, uint32_t pb, uint32_t& x0, uint32_t& x1,
                                           const EncTab& T, uint32_t& bits, Emit& em) {
     const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+    // count-only passes: the chunk's nb summed as packed upper halves (<= 16 x 16)
+    constexpr bool PKB = FSEHIP_ENC_PKB && counts<MODE>() && !emits<MODE>();
+    uint32_t bacc = 0;
     // all 16 symbol transforms depend only on the chunk: issue their LDS
     // reads up front so only the stateTable reads sit on the state chain
     uint2 t0[8], t1[8];
@@ -286,32 +324,39 @@ __device__ __forceinline__ void enc_chunk(const uint4& q, uint32_t c8, uint32_t 
             if (!FULL && c8 + (uint32_t)j >= pb) continue;
             const uint2 t = (j & 1) ? t1[j >> 1] : t0[j >> 1];
             const uint32_t v0 = x0;
-            const uint32_t nb0 = (t.x + x0) >> 16;
-            x0 = st_at(((x0 >> nb0) << 1) + t.y);
-            if (counts<MODE>()) bits += nb0;
+            const uint32_t s0 = state_step(x0, t);
+            const uint32_t nb0 = s0 >> 16;
+            if (counts<MODE>()) {
+                if (PKB) bacc = pk_add16(bacc, s0);
+                else bits += nb0;
+            }
             if (emits<MODE>()) {
                 em.put(__builtin_amdgcn_ubfe(v0, 0u, nb0), nb0);
                 if (j & 1) em.flush();  // <= 2 x 12 bits between flushes
             }
         }
         if (emits<MODE>()) em.flush();
+        if (PKB) bits += bacc >> 16;
         return;
     }
 #pragma unroll
     for (int j = 7; j >= 0; --j) {
         if (!FULL && c8 + (uint32_t)j >= pb) continue;
         const uint32_t v1 = x1, v0 = x0;
-        const uint32_t nb1 = (t1[j].x + x1) >> 16;
-        x1 = st_at(((x1 >> nb1) << 1) + t1[j].y);
-        const uint32_t nb0 = (t0[j].x + x0) >> 16;
-        x0 = st_at(((x0 >> nb0) << 1) + t0[j].y);
-        if (counts<MODE>()) bits += nb1 + nb0;
+        const uint32_t s1 = state_step(x1, t1[j]);
+        const uint32_t s0 = state_step(x0, t0[j]);
+        const uint32_t nb1 = s1 >> 16, nb0 = s0 >> 16;
+        if (counts<MODE>()) {
+            if (PKB) bacc = pk_add16(pk_add16(bacc, s1), s0);
+            else bits += nb1 + nb0;
+        }
         if (emits<MODE>()) {
             const uint32_t pairbits = (__builtin_amdgcn_ubfe(v0, 0u, nb0) << nb1) | __builtin_amdgcn_ubfe(v1, 0u, nb1);
             em.put(pairbits, nb1 + nb0);
             em.flush();
         }
     }
+    if (PKB) bits += bacc >> 16;
 }
 
 // Sidecar entry for the decoder state before pair p (= encoder state after
