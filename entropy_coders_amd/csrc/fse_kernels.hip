@@ -237,41 +237,45 @@ constexpr bool counts() { return MODE == PASS_COUNT || MODE == PASS_REPAIR || MO
 // state only until it meets the recorded trajectory: from there on states
 // and bits are identical, so the lane's total follows from the record and
 // its end state (its neighbour's start) is unchanged.
-// Slots hold {x0 | x1 << 16, bits still to come after the slot}: a pass
-// writes its running count there, and track_fixup turns the slots it wrote
-// into remaining counts once the pass total is known, so every slot stays
-// consistent with the lane's current trajectory.
+// Slots hold x0 | x1 << 16 (cx) and, per chain, the bits still to come
+// after the slot (cb: .x chain 0, .y chain 1): a pass writes its running
+// counts there, and track_fixup turns the slots it wrote into remaining
+// counts once the pass totals are known, so every slot stays consistent
+// with the lane's current trajectory.  Per-chain counts let a repair stop
+// each chain where it meets its record (enc_repair2).
 // Trajectory slots per lane.  16 (repairs stop sooner) measured slower
 // than 8 on C2: the count pass writes twice as many slots.
 constexpr uint32_t TRACK_SLOTS = 8;
 struct Track {
-    uint2* cp;        // this lane's slots (LDS)
+    uint32_t* cx;     // this lane's slots: state pairs (LDS)
+    uint2* cb;        // this lane's slots: per-chain bit counts (LDS)
     uint32_t ckc;     // chunks per slot
     bool done;        // REPAIR: met the recorded trajectory
     uint32_t jstar;   // REPAIR: the slot where it did (slots above it were rewritten)
 };
 
-// After a pass with total `total`: slots above `jlo` (exclusive) hold
+// After a pass with totals t0 / t1: slots above `jlo` (exclusive) hold
 // running counts; make them remaining counts.
-__device__ __forceinline__ void track_fixup(Track& tr, uint32_t nslot, int32_t jlo, uint32_t total) {
-    for (int32_t j = (int32_t)nslot - 1; j > jlo; --j) tr.cp[j].y = total - tr.cp[j].y;
+__device__ __forceinline__ void track_fixup(Track& tr, uint32_t nslot, int32_t jlo, uint32_t t0, uint32_t t1) {
+    for (int32_t j = (int32_t)nslot - 1; j > jlo; --j) {
+        const uint2 r = tr.cb[j];
+        tr.cb[j] = make_uint2(t0 - r.x, t1 - r.y);
+    }
 }
 
 struct EncState {
-    uint32_t x0, x1, bits;
+    uint32_t x0, x1, b0, b1;  // states; bits of chain 0 / chain 1 (NS = 1: b0 only)
 };
 
 // One state step on the dependent chain x -> stateTable[(x >> nb) + dFS],
 // nb = (deltaNbBits + x) >> 16: updates x and returns the sum deltaNbBits + x,
-// whose upper word is nb.  FSEHIP_ENC_SDWA: the shift takes nb as the sum's
-// upper word (SDWA src0_sel:WORD_1), so no VALU op computes nb on the chain
-// (add, shift, shift-add, ds_read_u16); callers take nb = sum >> 16 (or add
-// sums as packed halves, FSEHIP_ENC_PKB) off the chain.
+// whose upper word is nb.  Callers take nb = sum >> 16, or (counting passes)
+// add the sums as packed 16-bit halves, so that nb's only use on the chain
+// is the shift and the compiler takes it as the sum's upper word there (SDWA
+// src0_sel:WORD_1): add, shift, shift-add, ds_read_u16.  FSEHIP_ENC_SDWA
+// forces that shift in every pass (A/B knob, measured no faster).
 #ifndef FSEHIP_ENC_SDWA
 #define FSEHIP_ENC_SDWA 0
-#endif
-#ifndef FSEHIP_ENC_PKB
-#define FSEHIP_ENC_PKB 0
 #endif
 __device__ __forceinline__ uint32_t state_step(uint32_t& x, const uint2 t) {
     const uint32_t sum = t.x + x;
@@ -304,11 +308,12 @@ __device__ __forceinline__ uint32_t enc_step(uint32_t& x, uint32_t s, const EncT
 // of the topmost lane can extend past the last main-loop step pb.
 template <int MODE, bool FULL, int NS>
 __device__ __forceinline__ void enc_chunk(const uint4& q, uint32_t c8, uint32_t pb, uint32_t& x0, uint32_t& x1,
-                                          const EncTab& T, uint32_t& bits, Emit& em) {
+                                          const EncTab& T, uint32_t& b0, uint32_t& b1, Emit& em) {
     const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-    // count-only passes: the chunk's nb summed as packed upper halves (<= 16 x 16)
-    constexpr bool PKB = FSEHIP_ENC_PKB && counts<MODE>() && !emits<MODE>();
-    uint32_t bacc = 0;
+    // counting passes: each chain's nb summed as packed upper halves of its
+    // step sums (<= 16 x 16 per chunk), folded in once per chunk
+    constexpr bool PKB = counts<MODE>();
+    uint32_t bacc0 = 0, bacc1 = 0;
     // all 16 symbol transforms depend only on the chunk: issue their LDS
     // reads up front so only the stateTable reads sit on the state chain
     uint2 t0[8], t1[8];
@@ -326,17 +331,14 @@ __device__ __forceinline__ void enc_chunk(const uint4& q, uint32_t c8, uint32_t 
             const uint32_t v0 = x0;
             const uint32_t s0 = state_step(x0, t);
             const uint32_t nb0 = s0 >> 16;
-            if (counts<MODE>()) {
-                if (PKB) bacc = pk_add16(bacc, s0);
-                else bits += nb0;
-            }
+            if (PKB) bacc0 = pk_add16(bacc0, s0);
             if (emits<MODE>()) {
                 em.put(__builtin_amdgcn_ubfe(v0, 0u, nb0), nb0);
                 if (j & 1) em.flush();  // <= 2 x 12 bits between flushes
             }
         }
         if (emits<MODE>()) em.flush();
-        if (PKB) bits += bacc >> 16;
+        if (PKB) b0 += bacc0 >> 16;
         return;
     }
 #pragma unroll
@@ -346,9 +348,9 @@ __device__ __forceinline__ void enc_chunk(const uint4& q, uint32_t c8, uint32_t 
         const uint32_t s1 = state_step(x1, t1[j]);
         const uint32_t s0 = state_step(x0, t0[j]);
         const uint32_t nb1 = s1 >> 16, nb0 = s0 >> 16;
-        if (counts<MODE>()) {
-            if (PKB) bacc = pk_add16(pk_add16(bacc, s1), s0);
-            else bits += nb1 + nb0;
+        if (PKB) {
+            bacc1 = pk_add16(bacc1, s1);
+            bacc0 = pk_add16(bacc0, s0);
         }
         if (emits<MODE>()) {
             const uint32_t pairbits = (__builtin_amdgcn_ubfe(v0, 0u, nb0) << nb1) | __builtin_amdgcn_ubfe(v1, 0u, nb1);
@@ -356,7 +358,10 @@ __device__ __forceinline__ void enc_chunk(const uint4& q, uint32_t c8, uint32_t 
             em.flush();
         }
     }
-    if (PKB) bits += bacc >> 16;
+    if (PKB) {
+        b0 += bacc0 >> 16;
+        b1 += bacc1 >> 16;
+    }
 }
 
 // Sidecar entry for the decoder state before pair p (= encoder state after
@@ -398,7 +403,7 @@ __device__ __forceinline__ EncState enc_range(const uint8_t* __restrict__ blk, u
                                               EncState st, const EncTab& T, Emit& em, Ckpt& ck, Track& tr) {
     constexpr bool TRACK = counts<MODE>();
     constexpr bool RP = MODE == PASS_REPAIR || MODE == PASS_EREPAIR;
-    uint32_t x0 = st.x0, x1 = st.x1, bits = st.bits;
+    uint32_t x0 = st.x0, x1 = st.x1, b0 = st.b0, b1 = st.b1;
     if (pb <= pa) return st;
     const uint4* v = reinterpret_cast<const uint4*>(blk);
     constexpr uint32_t CS = NS == 2 ? 3u : 4u;  // log2 steps per 16-byte chunk
@@ -414,16 +419,19 @@ __device__ __forceinline__ EncState enc_range(const uint8_t* __restrict__ blk, u
         if (rem == 0u) {
             const uint32_t sv = x0 | (x1 << 16);
             if (RP) {
-                const uint2 r = tr.cp[slot];
-                if (r.x == sv) {
+                if (tr.cx[slot] == sv) {
+                    const uint2 r = tr.cb[slot];
                     tr.done = true;
                     tr.jstar = slot;
-                    bits += r.y;  // the rest of the trajectory is the recorded one
+                    b0 += r.x;  // the rest of the trajectory is the recorded one
+                    b1 += r.y;
                 } else {
-                    tr.cp[slot] = make_uint2(sv, bits);
+                    tr.cx[slot] = sv;
+                    tr.cb[slot] = make_uint2(b0, b1);
                 }
             } else {
-                tr.cp[slot] = make_uint2(sv, bits);
+                tr.cx[slot] = sv;
+                tr.cb[slot] = make_uint2(b0, b1);
             }
             slot -= 1u;
             rem = tr.ckc - 1u;
@@ -433,14 +441,14 @@ __device__ __forceinline__ EncState enc_range(const uint8_t* __restrict__ blk, u
     };
     if (pb & ((1u << CS) - 1u)) {  // partial topmost chunk
         const uint4 q = load_chunk(blk, n, (uint32_t)c_hi);
-        enc_chunk<MODE, false, NS>(q, (uint32_t)c_hi << CS, pb, x0, x1, T, bits, em);
+        enc_chunk<MODE, false, NS>(q, (uint32_t)c_hi << CS, pb, x0, x1, T, b0, b1, em);
         if (emits<MODE>()) em.drain();
         if (MODE == PASS_EMIT && ck.base && (((uint32_t)c_hi << CS) & ck.mask) == 0u)
             ckpt_record<NS>(ck, (uint32_t)c_hi << CS, em.pos(), x0, x1);
         if (TRACK) track();
         c_hi -= 1;
     }
-    if (c_hi < c_lo || (RP && tr.done)) return EncState{x0, x1, bits};
+    if (c_hi < c_lo || (RP && tr.done)) return EncState{x0, x1, b0, b1};
     auto ld = [&](int32_t c) { return v[c < c_lo ? c_lo : c]; };
     // source chunks in flight: PF - 1 ahead of the one being encoded
     constexpr int PF = emits<MODE>() ? FSEHIP_ENC_PF : 4;
@@ -448,7 +456,7 @@ __device__ __forceinline__ EncState enc_range(const uint8_t* __restrict__ blk, u
 #pragma unroll
     for (int k = 0; k < PF; ++k) q[k] = ld(c_hi - k);
     auto body = [&](const uint4& q, int32_t c) {
-        enc_chunk<MODE, true, NS>(q, (uint32_t)c << CS, pb, x0, x1, T, bits, em);
+        enc_chunk<MODE, true, NS>(q, (uint32_t)c << CS, pb, x0, x1, T, b0, b1, em);
         if (emits<MODE>()) em.drain();
         if (MODE == PASS_EMIT && ck.base && (((uint32_t)c << CS) & ck.mask) == 0u)
             ckpt_record<NS>(ck, (uint32_t)c << CS, em.pos(), x0, x1);
@@ -468,7 +476,94 @@ __device__ __forceinline__ EncState enc_range(const uint8_t* __restrict__ blk, u
         }
         if (done) break;
     }
-    return EncState{x0, x1, bits};
+    return EncState{x0, x1, b0, b1};
+}
+
+// Per-chain repair (NS = 2) of a lane below the top lane (whole chunks: S is
+// a multiple of 8).  The two states are independent chains (lib.rs:167-176),
+// so each chain whose start changed (bad0 / bad1) re-encodes from x0 / x1
+// only until it meets its own recorded trajectory at a slot, and a chunk
+// runs both chains while some lane of the wave still needs each, otherwise
+// only the one still needed (half the LDS gathers).  (A packed-pair test ran
+// both chains to the later of the two meetings, and both again when only
+// one start had changed: tools/chain_repair_sim.py.)  On return, for a chain
+// that was bad: tot_c = its bits over the lane; jc = the slot where it met
+// its record (-1: never, x_c is then its new end state); its slots above jc
+// hold running counts for the caller's fixup.
+// Measured slower (profiles/r05/enc_chain/enc_pc.txt): C2 1.64 against
+// 1.56 ms, skewed L = 12 6.87 against 5.90.  The step is latency-bound: a
+// chunk of one chain leaves each step's stateTable read with no second
+// chain to overlap, so it takes about as long as a chunk of both, and the
+// gathers it saves were not what the time waited on.  Off by default.
+#ifndef FSEHIP_ENC_PC
+#define FSEHIP_ENC_PC 0  // 1: per-chain repair (A/B); 0: packed-pair repair
+#endif
+template <int C>
+__device__ __forceinline__ void enc_chunk1(const uint4& q, uint32_t& x, uint32_t& b, const EncTab& T) {
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+    uint2 t[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t[j] = T.tt[(w[j >> 1] >> (16u * (uint32_t)(j & 1) + 8u * C)) & 0xFFu];
+    uint32_t bacc = 0;
+#pragma unroll
+    for (int j = 7; j >= 0; --j) bacc = pk_add16(bacc, state_step(x, t[j]));
+    b += bacc >> 16;
+}
+
+__device__ __forceinline__ void enc_repair2(const uint8_t* __restrict__ blk, uint32_t pa, uint32_t pb, uint32_t& x0,
+                                            uint32_t& x1, bool bad0, bool bad1, const EncTab& T, Track& tr,
+                                            uint32_t& tot0, uint32_t& tot1, int32_t& j0, int32_t& j1) {
+    const uint4* v = reinterpret_cast<const uint4*>(blk);
+    const int32_t c_hi = (int32_t)((pb - 1u) >> 3), c_lo = (int32_t)(pa >> 3);
+    uint32_t rem = (uint32_t)(c_hi - c_lo) % tr.ckc, slot = (uint32_t)(c_hi - c_lo) / tr.ckc;
+    bool d0 = !bad0, d1 = !bad1;
+    j0 = j1 = -1;
+    uint32_t b0 = 0, b1 = 0;
+    Emit em;  // not written by counting chunks
+    auto ld = [&](int32_t c) { return v[c < c_lo ? c_lo : c]; };
+    uint4 q[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) q[k] = ld(c_hi - k);
+    for (int32_t c = c_hi;; c -= 4) {
+        bool out = false;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const bool n0 = __ballot(!d0) != 0ull, n1 = __ballot(!d1) != 0ull;  // wave-uniform
+            if (n0 && n1) enc_chunk<PASS_COUNT, true, 2>(q[k], 0u, pb, x0, x1, T, b0, b1, em);
+            else if (n0) enc_chunk1<0>(q[k], x0, b0, T);
+            else enc_chunk1<1>(q[k], x1, b1, T);
+            if (rem == 0u) {
+                const uint32_t r = tr.cx[slot];
+                const uint2 rb = tr.cb[slot];
+                if (!d0 && (r & 0xFFFFu) == x0) {  // from here on chain 0 is the recorded one
+                    d0 = true;
+                    j0 = (int32_t)slot;
+                    tot0 = b0 + rb.x;
+                }
+                if (!d1 && (r >> 16) == x1) {
+                    d1 = true;
+                    j1 = (int32_t)slot;
+                    tot1 = b1 + rb.y;
+                }
+                if (!d0 || !d1) {  // the chains still off their record rewrite their halves
+                    tr.cx[slot] = (d0 ? r & 0xFFFFu : x0) | (d1 ? r & 0xFFFF0000u : x1 << 16);
+                    tr.cb[slot] = make_uint2(d0 ? rb.x : b0, d1 ? rb.y : b1);
+                }
+                slot -= 1u;
+                rem = tr.ckc - 1u;
+            } else {
+                rem -= 1u;
+            }
+            if ((d0 && d1) || c - k - 1 < c_lo) {
+                out = true;
+                break;
+            }
+            q[k] = ld(c - k - 4);
+        }
+        if (out) break;
+    }
+    if (!d0) tot0 = b0;  // never met its record: the whole lane recounted
+    if (!d1) tot1 = b1;
 }
 
 // Encoder::new_first_symbol, fse.rs:210-218
@@ -486,7 +581,7 @@ __device__ __forceinline__ uint32_t enc_init(const EncTab& T, uint32_t s) {
 template <int MODE, int NS>
 __device__ __forceinline__ EncState top_start(const uint8_t* blk, uint32_t n, const EncTab& tab, Emit& em) {
     EncState e;
-    e.bits = 0;
+    e.b0 = e.b1 = 0;
     if (NS == 1) {
         e.x0 = enc_init(tab, blk[n - 1u]);
         e.x1 = 0;  // unused; 0 in every lane so packed states compare equal
@@ -497,7 +592,7 @@ __device__ __forceinline__ EncState top_start(const uint8_t* blk, uint32_t n, co
         e.x1 = enc_init(tab, blk[n - 2u]);
         const uint32_t v0 = e.x0;
         const uint32_t nb = enc_step(e.x0, blk[n - 3u], tab);
-        if (MODE == PASS_COUNT) e.bits = nb;
+        if (MODE == PASS_COUNT) e.b0 = nb;
         if (MODE == PASS_EMIT) {
             em.put(v0 & ((1u << nb) - 1u), nb);
             em.flush();
@@ -547,8 +642,9 @@ struct EncSmem {
         // the boundary-word merge after it
         union {
             struct {
-                uint2 cp[64 * TRACK_SLOTS];  // count-pass trajectories (Track)
-                uint32_t cntF[BPW][T + 1];   // each lane's end state
+                uint2 cb[64 * TRACK_SLOTS];     // trajectories (Track): per-chain bit counts
+                uint32_t cx[64 * TRACK_SLOTS];  // and state pairs
+                uint32_t cntF[BPW][T + 1];      // each lane's end state
             } u;
             __attribute__((aligned(16))) uint32_t ring[64 * RING_STRIDE];  // emit: output ring per lane (Emit)
             struct {
@@ -712,10 +808,13 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     // start until the recorded trajectory is met) until the fixed point, then
     // the emit pass writes straight to the final offsets.  A repair round
     // costs the slowest lane's convergence distance.
-    Track tr{&sm.ph.p2.u.cp[lane * TRACK_SLOTS], max(1u, (S / SPC + TRACK_SLOTS - 1u) / TRACK_SLOTS), false, 0u};
+    Track tr{&sm.ph.p2.u.cx[lane * TRACK_SLOTS], &sm.ph.p2.u.cb[lane * TRACK_SLOTS],
+             max(1u, (S / SPC + TRACK_SLOTS - 1u) / TRACK_SLOTS), false, 0u};
     const uint32_t nslot = pb > pa ? (((pb - 1u) / SPC) - (pa / SPC)) / tr.ckc + 1u : 0u;
     uint32_t start = (1u << L) | (NS == 2 ? (1u << L) << 16 : 0u);
     uint32_t bits = 0;
+    uint32_t tot0 = 0, tot1 = 0;  // the lane's bits per chain
+    uint32_t myF = 0;             // the lane's end state (cntF)
     uint32_t n_iter = 0, n_rerun = 0;  // diagnostics (stamps counters)
     {
         // count pass: the top lane from its exact start (init states + the
@@ -729,39 +828,67 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
         constexpr int MC = PASS_COUNT, MR = PASS_REPAIR;
 #endif
         if (act) {
-            EncState e0 = (k == ktop) ? top_start<PASS_COUNT, NS>(blk, n, tab, em) : EncState{start & 0xFFFFu, start >> 16, 0u};
+            EncState e0 = (k == ktop) ? top_start<PASS_COUNT, NS>(blk, n, tab, em)
+                                      : EncState{start & 0xFFFFu, start >> 16, 0u, 0u};
             e0 = enc_range<MC, NS>(blk, n, pa, pb, e0, tab, em, ck, tr);
-            bits = e0.bits;
-            sm.ph.p2.u.cntF[b][k] = e0.x0 | (e0.x1 << 16);
-            track_fixup(tr, nslot, -1, bits);
+            tot0 = e0.b0;
+            tot1 = e0.b1;
+            myF = e0.x0 | (e0.x1 << 16);
+            sm.ph.p2.u.cntF[b][k] = myF;
+            track_fixup(tr, nslot, -1, tot0, tot1);
         }
         FSE_STAMP(P, 5);
+        constexpr bool PC = NS == 2 && FSEHIP_ENC_PC && !(FSEHIP_ENC_ABL & 2);
         for (;;) {
             if (P.debug & 16u) break;  // ablation: no repair (wrong output)
             __syncthreads();
-            bool bad = false;
+            bool bad0 = false, bad1 = false;
             uint32_t nbF = 0;
             if (act && k < ktop) {
                 nbF = sm.ph.p2.u.cntF[b][k + 1];
-                bad = nbF != start;
+                bad0 = ((nbF ^ start) & 0xFFFFu) != 0u;
+                bad1 = ((nbF ^ start) >> 16) != 0u;
             }
+            const bool bad = bad0 || bad1;
             __syncthreads();
             if (__ballot(bad) == 0) break;
             ++n_iter;
             n_rerun += (uint32_t)__popcll(__ballot(bad));
             if (bad) {
                 start = nbF;
-                tr.done = false;
+                if constexpr (PC) {
+                    uint32_t x0 = start & 0xFFFFu, x1 = start >> 16;
+                    int32_t j0, j1;
+                    enc_repair2(blk, pa, pb, x0, x1, bad0, bad1, tab, tr, tot0, tot1, j0, j1);
+                    const bool nc0 = bad0 && j0 < 0, nc1 = bad1 && j1 < 0;  // met no record: a new end state
+                    if (nc0 || nc1) {
+                        myF = (nc0 ? x0 : myF & 0xFFFFu) | (nc1 ? x1 << 16 : myF & 0xFFFF0000u);
+                        sm.ph.p2.u.cntF[b][k] = myF;
+                    }
+                    for (int32_t j = (int32_t)nslot - 1; j >= 0; --j) {  // running -> remaining counts
+                        uint2 r = tr.cb[j];
+                        if (bad0 && j > j0) r.x = tot0 - r.x;
+                        if (bad1 && j > j1) r.y = tot1 - r.y;
+                        tr.cb[j] = r;
+                    }
+                } else {
+                    tr.done = false;
 #if FSEHIP_ENC_ABL & 2
-                em.start(nullptr, pa * 24u, 0u, &sm.ring2[lane * RING_STRIDE]);
+                    em.start(nullptr, pa * 24u, 0u, &sm.ring2[lane * RING_STRIDE]);
 #endif
-                const EncState e0 = enc_range<MR, NS>(blk, n, pa, pb, EncState{start & 0xFFFFu, start >> 16, 0u},
-                                                           tab, em, ck, tr);
-                bits = e0.bits;
-                if (!tr.done) sm.ph.p2.u.cntF[b][k] = e0.x0 | (e0.x1 << 16);  // did not converge: new end state
-                track_fixup(tr, nslot, tr.done ? (int32_t)tr.jstar : -1, bits);
+                    const EncState e0 = enc_range<MR, NS>(blk, n, pa, pb,
+                                                          EncState{start & 0xFFFFu, start >> 16, 0u, 0u}, tab, em, ck, tr);
+                    tot0 = e0.b0;
+                    tot1 = e0.b1;
+                    if (!tr.done) {  // did not converge: new end state
+                        myF = e0.x0 | (e0.x1 << 16);
+                        sm.ph.p2.u.cntF[b][k] = myF;
+                    }
+                    track_fixup(tr, nslot, tr.done ? (int32_t)tr.jstar : -1, tot0, tot1);
+                }
             }
         }
+        bits = tot0 + tot1;
         if (k == 0) bits += (uint32_t)NS * L + 1u;  // finals + marker (lib.rs:178-181 / 139-141)
     }
 
