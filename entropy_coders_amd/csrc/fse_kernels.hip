@@ -364,6 +364,76 @@ __device__ __forceinline__ void enc_chunk(const uint4& q, uint32_t c8, uint32_t 
     }
 }
 
+// The same chunk with its symbol transforms already in t0 / t1 (loaded one
+// chunk ahead): each pair's two transforms are reloaded from the next
+// chunk's words qn as soon as the pair has used them, so the next chunk
+// starts with its transforms landed instead of waiting for 16 LDS reads
+// (the state loop is latency-bound: that wait was one exposed LDS round
+// trip per 8 pairs).  Same registers, same instruction count.
+#ifndef FSEHIP_ENC_TTPF
+#define FSEHIP_ENC_TTPF 1
+#endif
+__device__ __forceinline__ void tt_load(const uint4& q, uint2 (&t0)[8], uint2 (&t1)[8], const EncTab& T) {
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint32_t sh = 16u * (uint32_t)(j & 1);
+        t0[j] = T.tt[(w[j >> 1] >> sh) & 0xFFu];
+        t1[j] = T.tt[(w[j >> 1] >> (sh + 8u)) & 0xFFu];
+    }
+}
+template <int MODE, int NS>
+__device__ __forceinline__ void enc_chunk_pl(const uint4& qn, uint2 (&t0)[8], uint2 (&t1)[8], uint32_t& x0,
+                                             uint32_t& x1, const EncTab& T, uint32_t& b0, uint32_t& b1, Emit& em) {
+    const uint32_t wn[4] = {qn.x, qn.y, qn.z, qn.w};
+    constexpr bool PKB = counts<MODE>();
+    uint32_t bacc0 = 0, bacc1 = 0;
+    auto reload = [&](int j) {
+        const uint32_t sh = 16u * (uint32_t)(j & 1);
+        t0[j] = T.tt[(wn[j >> 1] >> sh) & 0xFFu];
+        t1[j] = T.tt[(wn[j >> 1] >> (sh + 8u)) & 0xFFu];
+    };
+    if (NS == 1) {
+#pragma unroll
+        for (int j = 15; j >= 0; --j) {
+            const uint2 t = (j & 1) ? t1[j >> 1] : t0[j >> 1];
+            const uint32_t v0 = x0;
+            const uint32_t s0 = state_step(x0, t);
+            const uint32_t nb0 = s0 >> 16;
+            if (PKB) bacc0 = pk_add16(bacc0, s0);
+            if (emits<MODE>()) {
+                em.put(__builtin_amdgcn_ubfe(v0, 0u, nb0), nb0);
+                if (j & 1) em.flush();  // <= 2 x 12 bits between flushes
+            }
+            if ((j & 1) == 0) reload(j >> 1);
+        }
+        if (emits<MODE>()) em.flush();
+        if (PKB) b0 += bacc0 >> 16;
+        return;
+    }
+#pragma unroll
+    for (int j = 7; j >= 0; --j) {
+        const uint32_t v1 = x1, v0 = x0;
+        const uint32_t s1 = state_step(x1, t1[j]);
+        const uint32_t s0 = state_step(x0, t0[j]);
+        reload(j);
+        const uint32_t nb1 = s1 >> 16, nb0 = s0 >> 16;
+        if (PKB) {
+            bacc1 = pk_add16(bacc1, s1);
+            bacc0 = pk_add16(bacc0, s0);
+        }
+        if (emits<MODE>()) {
+            const uint32_t pairbits = (__builtin_amdgcn_ubfe(v0, 0u, nb0) << nb1) | __builtin_amdgcn_ubfe(v1, 0u, nb1);
+            em.put(pairbits, nb1 + nb0);
+            em.flush();
+        }
+    }
+    if (PKB) {
+        b0 += bacc0 >> 16;
+        b1 += bacc1 >> 16;
+    }
+}
+
 // Sidecar entry for the decoder state before pair p (= encoder state after
 // encoding pair p): bit position (payload-relative) and both states.
 // (NS = 1: one state, s1 = 0.)
@@ -455,8 +525,19 @@ __device__ __forceinline__ EncState enc_range(const uint8_t* __restrict__ blk, u
     uint4 q[PF];
 #pragma unroll
     for (int k = 0; k < PF; ++k) q[k] = ld(c_hi - k);
-    auto body = [&](const uint4& q, int32_t c) {
+#if FSEHIP_ENC_TTPF
+    uint2 t0[8], t1[8];  // the transforms of the chunk being encoded (tt_load / enc_chunk_pl)
+    tt_load(q[0], t0, t1, T);
+#endif
+    // qn: the next chunk's words (already loaded: PF - 1 chunks ahead)
+    auto body = [&](const uint4& q, const uint4& qn, int32_t c) {
+#if FSEHIP_ENC_TTPF
+        (void)q;
+        enc_chunk_pl<MODE, NS>(qn, t0, t1, x0, x1, T, b0, b1, em);
+#else
+        (void)qn;
         enc_chunk<MODE, true, NS>(q, (uint32_t)c << CS, pb, x0, x1, T, b0, b1, em);
+#endif
         if (emits<MODE>()) em.drain();
         if (MODE == PASS_EMIT && ck.base && (((uint32_t)c << CS) & ck.mask) == 0u)
             ckpt_record<NS>(ck, (uint32_t)c << CS, em.pos(), x0, x1);
@@ -467,7 +548,7 @@ __device__ __forceinline__ EncState enc_range(const uint8_t* __restrict__ blk, u
         bool done = false;
 #pragma unroll
         for (int k = 0; k < PF; ++k) {
-            body(q[k], c - k);
+            body(q[k], q[(k + 1) % PF], c - k);
             if (stop(c - k - 1)) {
                 done = true;
                 break;
