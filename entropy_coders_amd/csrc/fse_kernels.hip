@@ -98,6 +98,9 @@ struct Emit {
     bool skip_head;
     uint32_t* gw;
     uint32_t* ring;     // LDS, RING_WORDS words, 16-byte aligned
+#if FSEHIP_ENC_ABL & 192
+    uint32_t probe = 0;  // LDS-split probes: their reads folded in here (never waited for per pair)
+#endif
     __device__ __forceinline__ void start(uint32_t* g, uint32_t off, uint32_t lim = 0xFFFFFFFFu,
                                           uint32_t* r = nullptr) {
         gw = g;
@@ -416,6 +419,18 @@ __device__ __forceinline__ void enc_chunk_pl(const uint4& qn, uint2 (&t0)[8], ui
         const uint32_t v1 = x1, v0 = x0;
         const uint32_t s1 = state_step(x1, t1[j]);
         const uint32_t s0 = state_step(x0, t0[j]);
+#if FSEHIP_ENC_ABL & 64  // LDS-split probe: one more stateTable gather per pair (chain 0's, one bank over; sunk)
+        {
+            const uint32_t a = (((v0 >> (s0 >> 16)) << 1) + t0[j].y) ^ 4u;
+            em.probe ^= st_at(a);
+        }
+#endif
+#if FSEHIP_ENC_ABL & 128  // LDS-split probe: one more transform gather per pair (the neighbour symbol's; sunk)
+        {
+            const uint2 e = T.tt[((wn[j >> 1] >> (16u * (uint32_t)(j & 1))) & 0xFFu) ^ 1u];
+            em.probe ^= e.x ^ e.y;
+        }
+#endif
         reload(j);
         const uint32_t nb1 = s1 >> 16, nb0 = s0 >> 16;
         if (PKB) {
@@ -1085,6 +1100,9 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
         if (fits) {
             P.status[gb] = FSE_OK;
             P.comp_len[gb] = (total_bits + 7u) >> 3;
+#if FSEHIP_ENC_ABL & 192
+            if (em.probe == 0x9E37u + (uint32_t)P.n_blocks * 0x10000u) P.comp_len[gb] = 0;  // keeps the probe reads (never true)
+#endif
             if (P.payload_bits) P.payload_bits[gb] = total_bits - hdr_bits;
         } else {
             P.status[gb] = FSE_ERR_DST_TOO_SMALL;

@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round 5, call W: what one more LDS gather per pair costs the encoder in
+# time when nothing waits for it (the probes' reads are folded into a
+# register checked once at the end): product vs FSEHIP_ENC_ABL=64 (one more
+# stateTable gather per pair) and 128 (one more transform gather), C2
+# encode, three rounds; then one SQ counter pass over each probe.
+set -o pipefail
+O=gpurun_out/r05_w
+mkdir -p $O
+for i in 1 2 3; do
+  for v in libfsehip.so libfsehip_est.so libfsehip_ett.so; do
+    FSEHIP_LIB=$v timeout -k 10 180 python3 tools/enc_ab.py 2>&1 | grep -v amdgpu.ids | tee -a $O/enc_split_time.txt || exit 1
+  done
+done
+for v in libfsehip_est.so libfsehip_ett.so; do
+  FSEHIP_LIB=$v PROF_NO_SERIAL=1 PROF_NO_C3=1 timeout -k 10 300 tools/lds_pass.sh $O/lds_$v > $O/lds_$v.log 2>&1 || { tail -20 $O/lds_$v.log; exit 1; }
+  python3 tools/lds_summary.py $O/lds_$v > $O/lds_$v.txt 2>&1 || { cat $O/lds_$v.txt; exit 1; }
+  echo "== $v"; grep -E "encode_blocks " $O/lds_$v.txt || true
+done
