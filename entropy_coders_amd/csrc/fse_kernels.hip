@@ -1269,10 +1269,11 @@ hipError_t launch_encode(const EncParams& P, uint32_t lmax, hipStream_t stream) 
         else if (lmax <= 14) go(encode_blocks_kernel<14, 64, 1>);
         else go(encode_blocks_kernel<15, 64, 1>);
     } else if (T == 64) {
-        // 11 workgroups per CU rather than the 12 its 12.6 KB allow: same
-        // time on C2, 5% less on near-uniform data (tools/occ_enc.py, one
-        // process: 12 -> 2.00 ms, 11 -> 1.90, 10 -> 1.88; C2 1.58 / 1.57 /
-        // 1.61), where the twelfth workgroup only adds contention
+        // 11 workgroups per CU rather than the 12 its 12.6 KB allowed in
+        // round 3: same time on C2, 5% less on near-uniform data
+        // (tools/occ_enc.py, one process: 12 -> 2.00 ms, 11 -> 1.90, 10 ->
+        // 1.88; C2 1.58 / 1.57 / 1.61), where the twelfth workgroup only adds
+        // contention.  (At 14.6 KB, round 5, 11 is also the most that fit.)
         static const uint32_t pad11 = [] {
             hipFuncAttributes fa{};
             if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(encode_blocks_kernel<11, 64, 2>)) != hipSuccess)
