@@ -280,6 +280,45 @@ struct LdsChain {
 #endif
         return __builtin_amdgcn_perm(e1, e0, 0x0c0c0501u);  // sym0 | sym1 << 8
     }
+    // Two pairs with one payload read: a pair takes <= 28 bits, so the
+    // second pair's window base is the first's (lo) or one word below it, and
+    // one ds_read2_b32 of words lo/32 - 1 and lo/32 serves both (the 16-byte
+    // pad below the image covers word -2).  One LDS instruction fewer per two
+    // pairs, and the second pair's address arithmetic is a select.
+    __device__ __forceinline__ void pair2(const uint32_t* pay, const uint8_t* dtb, uint32_t& ra, uint32_t& rb) {
+        const int32_t loA = (pos - PAIR_MAX_BITS) & ~31;
+        const uint32_t* wp = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(pay) + (loA >> 3) - 4);
+        const uint32_t q1 = wp[0], q0 = wp[1];  // words lo/32 - 1, lo/32
+        {
+            const uint32_t e0 = *reinterpret_cast<const uint32_t*>(dtb + a0);
+            const uint32_t e1 = *reinterpret_cast<const uint32_t*>(dtb + a1);
+            const uint32_t w1 = loA == B ? whi : wlo;
+            pos -= (int32_t)((e0 + e1) & 0xFFu);
+            const uint32_t x = (uint32_t)((((uint64_t)w1 << 32) | q0) >> (uint32_t)(pos - loA));
+            B = loA;
+            whi = w1;
+            wlo = q0;
+            a0 = (e0 >> 16) + (__builtin_amdgcn_ubfe(x, e1, e0) << 2);
+            a1 = (e1 >> 16) + (__builtin_amdgcn_ubfe(x, 0u, e1) << 2);
+            ra = __builtin_amdgcn_perm(e1, e0, 0x0c0c0501u);
+        }
+        {
+            const int32_t loB = (pos - PAIR_MAX_BITS) & ~31;  // loA or loA - 32
+            const uint32_t e0 = *reinterpret_cast<const uint32_t*>(dtb + a0);
+            const uint32_t e1 = *reinterpret_cast<const uint32_t*>(dtb + a1);
+            const bool same = loB == loA;
+            const uint32_t w1 = same ? whi : wlo;
+            const uint32_t w0 = same ? q0 : q1;
+            pos -= (int32_t)((e0 + e1) & 0xFFu);
+            const uint32_t x = (uint32_t)((((uint64_t)w1 << 32) | w0) >> (uint32_t)(pos - loB));
+            B = loB;
+            whi = w1;
+            wlo = w0;
+            a0 = (e0 >> 16) + (__builtin_amdgcn_ubfe(x, e1, e0) << 2);
+            a1 = (e1 >> 16) + (__builtin_amdgcn_ubfe(x, 0u, e1) << 2);
+            rb = __builtin_amdgcn_perm(e1, e0, 0x0c0c0501u);
+        }
+    }
     __device__ __forceinline__ uint32_t s0() const { return a0 >> 2; }
     __device__ __forceinline__ uint32_t s1() const { return a1 >> 2; }
     // decode-table entry of state s (Dte layout)
@@ -287,6 +326,30 @@ struct LdsChain {
         return *reinterpret_cast<const uint32_t*>(dtb + 4u * s);
     }
 };
+// pair2 in the group loops (A/B knob; the FSEHIP_ABL probes live in pair()).
+// Measured no faster (profiles/r05/dec_pair2/): C3 0.875-0.922 against
+// 0.885-0.918 ms, C2 decode 0.509-0.522 against 0.505-0.511, same box, exact
+// -- unlike the encoder, one LDS instruction fewer per two pairs (and half a
+// VALU op more) does not move the decoder.  Off by default.
+#ifndef FSEHIP_DEC_PAIR2
+#define FSEHIP_DEC_PAIR2 0
+#endif
+template <class Chain, class Tab>
+__device__ __forceinline__ uint32_t two_pairs(Chain& c, const uint32_t* pay, const Tab& dtb) {
+    const uint32_t lo = c.pair(pay, dtb);
+    const uint32_t hi = c.pair(pay, dtb);
+    return __builtin_amdgcn_perm(hi, lo, 0x05040100u);  // lo.b0 lo.b1 hi.b0 hi.b1
+}
+__device__ __forceinline__ uint32_t two_pairs(LdsChain& c, const uint32_t* pay, const uint8_t* const& dtb) {
+#if FSEHIP_DEC_PAIR2 && !FSEHIP_ABL
+    uint32_t lo, hi;
+    c.pair2(pay, dtb, lo, hi);
+#else
+    const uint32_t lo = c.pair(pay, dtb);
+    const uint32_t hi = c.pair(pay, dtb);
+#endif
+    return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+}
 
 // Bits [pos, pos + 32) of an LDS-staged block (pos >= 0): one ds_read2 of
 // the two words holding them and a v_alignbit (the end-of-block steps).
@@ -348,11 +411,7 @@ __device__ __forceinline__ void run_groups_tx(Chain& c, uint32_t my_ng, uint32_t
         uint32_t w[DEC_GROUP / 2u];
         if (g < my_ng) {
 #pragma unroll
-            for (uint32_t j = 0; j < DEC_GROUP; j += 2u) {
-                const uint32_t lo = c.pair(pay, dtb);
-                const uint32_t hi = c.pair(pay, dtb);
-                w[j >> 1] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
-            }
+            for (uint32_t j = 0; j < DEC_GROUP; j += 2u) w[j >> 1] = two_pairs(c, pay, dtb);
         } else {
 #pragma unroll
             for (uint32_t j = 0; j < DEC_GROUP / 2u; ++j) w[j] = 0;
@@ -408,11 +467,7 @@ __device__ __forceinline__ int32_t run_chain(Chain& c, const uint32_t* pay, cons
     for (; p + DEC_GROUP <= p1; p += DEC_GROUP) {
         uint32_t w[DEC_GROUP / 2u];
 #pragma unroll
-        for (uint32_t j = 0; j < DEC_GROUP; j += 2u) {
-            const uint32_t lo = c.pair(pay, dtb);
-            const uint32_t hi = c.pair(pay, dtb);
-            w[j >> 1] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);  // lo.b0 lo.b1 hi.b0 hi.b1
-        }
+        for (uint32_t j = 0; j < DEC_GROUP; j += 2u) w[j >> 1] = two_pairs(c, pay, dtb);
         store_group(out + 2u * p, w);
     }
     for (; p < p1; ++p) {
