@@ -144,10 +144,13 @@ __global__ __launch_bounds__(64) void table_kernel(const fse_norm_histogram* nh,
     const uint32_t size = 1u << L;
     int rc;
     if (enc) {
-        rc = wave_build_spread(norm, L, tl, sym_at, occ, cumul, cnt, [&](uint32_t i, uint32_t s, uint32_t r) {
-            et->table[cumul[s] + r] = (uint16_t)(size + i);  // fse.rs:157-162
-            et->symbols[i] = (uint8_t)s;
-        });
+        rc = wave_build_spread(
+            norm, L, tl, sym_at, occ, cumul, cnt,
+            [&](uint32_t i, uint32_t s, uint32_t r) {
+                et->table[r] = (uint16_t)(size + i);  // fse.rs:157-162 (r = cumul[s] + rank)
+                et->symbols[i] = (uint8_t)s;
+            },
+            [&](uint32_t s) { return (uint32_t)cumul[s]; });
         // symbol transforms (fse.rs:165-188); total before symbol s = cumul[s]
         for (uint32_t s = lane; s < 256u; s += WAVE) {
             uint32_t bits = 0;
@@ -171,14 +174,17 @@ __global__ __launch_bounds__(64) void table_kernel(const fse_norm_histogram* nh,
         if (lane == 0) et->table_log = L;
     } else {
         rc = wave_build_spread(norm, L, tl, sym_at, occ, cumul, cnt, [&](uint32_t i, uint32_t s, uint32_t r) {
-            const int32_t v = norm[s];
-            const uint32_t nx = (v < 0 ? 1u : (uint32_t)v) + r;  // symbol_next (fse.rs:296-308, 329-331)
+            const uint32_t nx = r;  // symbol_next + rank (fse.rs:296-308, 329-331)
             const uint32_t nb = L - ilog2u(nx);
             fse_decode_transform e;
             e.new_state = (uint16_t)((nx << nb) - size);
             e.symbol = (uint8_t)s;
             e.num_bits = (uint8_t)nb;
             dt->table[i] = e;
+        },
+        [&](uint32_t s) {
+            const int32_t v = norm[s];
+            return v < 0 ? 1u : (uint32_t)v;
         });
         uint32_t big = 0;  // fast_mode: no norm >= 2^(L-1) (fse.rs:302-305)
         for (uint32_t s = lane; s < tl; s += WAVE)

@@ -1012,15 +1012,17 @@ __global__ __launch_bounds__(64) void dtable_blocks_kernel(DtParams P) {
     if (rc == FSE_OK) {
         const uint32_t size = 1u << L;
         uint32_t* dt = P.dt + gb * (uint64_t)SIZE;
-        auto visit = [&](uint32_t i, uint32_t s, uint32_t r) {
-            const int32_t v = norm[s];
-            const uint32_t nx = (v < 0 ? 1u : (uint32_t)v) + r;
+        auto visit = [&](uint32_t i, uint32_t s, uint32_t nx) {  // nx = the symbol's first x + rank
             const uint32_t nb = L - ilog2u(nx);
             dt[i] = Dte<LMAX>::make(nb, s, (nx << nb) - size);
         };
+        auto first_x = [&](uint32_t s) {  // symbol_next (fse.rs:296-308): 1 for a -1 count
+            const int32_t v = norm[s];
+            return v < 0 ? 1u : (uint32_t)v;
+        };
         // two-pass ranks need 2^L / 64 per-chunk registers: up to L = 12
-        if (LMAX <= 12) rc = wave_build_spread<SIZE / 64u>(norm, L, tl, sym_at, occ, cumul, cnt, visit, rk, pm, &P);
-        else rc = wave_build_spread(norm, L, tl, sym_at, occ, cumul, cnt, visit);
+        if (LMAX <= 12) rc = wave_build_spread<SIZE / 64u>(norm, L, tl, sym_at, occ, cumul, cnt, visit, first_x, rk, pm, &P);
+        else rc = wave_build_spread(norm, L, tl, sym_at, occ, cumul, cnt, visit, first_x);
     }
     FSE_STAMP(P, 8);
     if (lane == 0) P.dtinfo[gb] = rc == FSE_OK ? (int32_t)((uint32_t)hl | (L << 16)) : rc;

@@ -685,9 +685,12 @@ __device__ inline int header_read_row(const lds_u32* row, uint32_t rot, uint32_t
 // wave-parallel.  After the call:
 //   sym_at[i]  = symbol at table position i            (LDS, 2^L bytes)
 //   cumul[s]   = sum_{t<s} c'(t), c' = 1 for -1         (LDS, 256)
-// and `visit(i, s, rank)` is invoked once per position with the rank of
-// position i among the positions holding s in ascending position order
-// (stateTable order, fse.rs:158-162; DecodeTable order, fse.rs:329-337).
+// and `visit(i, s, base(s) + rank)` is invoked once per position with the
+// rank of position i among the positions holding s in ascending position
+// order (stateTable order, fse.rs:158-162; DecodeTable order, fse.rs:329-337)
+// plus the caller's per-symbol base (cumul[s] for the stateTable, the
+// symbol's first x for the decode table), folded into the rank counters so
+// that a visit reads no per-symbol array.
 //
 // The spread walks multipliers m = 0..2^L-1: position (m*step) mod 2^L is
 // visited iff it is <= the high threshold, and the j-th visited position
@@ -707,9 +710,9 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t v) { return dpp0<0x138, 0
 struct NoStamps {
     uint64_t* stamps = nullptr;
 };
-template <uint32_t MAXCH = 64, typename Visit, class SP = NoStamps>  // MAXCH: 2^LMAX / 64 chunks (two-pass ranks)
+template <uint32_t MAXCH = 64, typename Visit, typename Base, class SP = NoStamps>  // MAXCH: 2^LMAX / 64 chunks (two-pass ranks)
 __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_t tl, uint8_t* sym_at,
-                                        uint8_t* occ_sym, uint16_t* cumul, uint32_t* cnt, Visit visit,
+                                        uint8_t* occ_sym, uint16_t* cumul, uint32_t* cnt, Visit visit, Base base,
                                         uint16_t* RK = nullptr, uint64_t* PM = nullptr, const SP* SPp = nullptr) {
     // SPp: diagnostics only, a params struct with `stamps` (phase stamps 3..7)
 #define SPREAD_STAMP(k)                                  \
@@ -745,7 +748,6 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
         reinterpret_cast<uint4*>(occ_sym)[i] = make_uint4(0, 0, 0, 0);
         reinterpret_cast<uint4*>(sym_at)[i] = make_uint4(0, 0, 0, 0);
     }
-    for (uint32_t s = lane; s < 256; s += WAVE) cnt[s] = 0;
     wave_sync();
     {
         uint32_t c = ex_c, p = ex_p, ng = ex_n;
@@ -795,10 +797,18 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
             }
             const uint32_t incl = wave_incl_sum(nv);
             uint32_t j = j0 + incl - nv;
+            // owners of occurrences j .. j + 3: one read of the two words
+            // holding them (a 2^L-byte array sits in a larger LDS region or
+            // at the end of LDS, where reads past it return 0)
+            const uint32_t ja = j & ~3u;
+            const uint32_t* o4 = reinterpret_cast<const uint32_t*>(occ_sym) + (ja >> 2);
+            const uint64_t ow = (((uint64_t)o4[1] << 32) | o4[0]) >> (8u * (j - ja));
+            uint32_t c = 0;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                if (v[k] && j < total_pos) sym_at[p[k]] = occ_sym[j];
+                if (v[k] && j < total_pos) sym_at[p[k]] = (uint8_t)(ow >> (8u * c));
                 j += v[k] ? 1u : 0u;
+                c += v[k] ? 1u : 0u;
             }
             j0 += bcast63(incl);
         }
@@ -828,9 +838,10 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
         }
         wave_sync();
         SPREAD_STAMP(6);
-        // per-symbol exclusive prefix over the chunks (lane = symbol)
+        // per-symbol exclusive prefix over the chunks (lane = symbol), from
+        // the symbol's base
         {
-            uint32_t run = 0;
+            uint32_t run = base(lane);
 #pragma unroll
             for (uint32_t t = 0; t < MAXCH; ++t) {
                 if (t < nch) {
@@ -858,8 +869,10 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
     // now, so the caller may alias the masks into it)
     const bool lds_match = PM != nullptr && tl <= 64u && size >= WAVE;
     const uint64_t lanebit = 1ull << lane;
-    for (uint32_t base = 0; base < size; base += WAVE) {
-        uint32_t i = base + lane;
+    for (uint32_t s = lane; s < 256; s += WAVE) cnt[s] = base(s);
+    wave_sync();
+    for (uint32_t i0 = 0; i0 < size; i0 += WAVE) {
+        uint32_t i = i0 + lane;
         bool act = i < size;
         uint64_t active = __ballot(act);
         uint32_t s = act ? sym_at[i] : 0u;

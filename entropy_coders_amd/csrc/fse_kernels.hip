@@ -815,10 +815,11 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
             const uint16_t* cumul = sm.ph.p1.cumul;
             rc = wave_build_spread(sm.ph.p1.norm, L, tl, sm.ph.p1.u.sym_at, reinterpret_cast<uint8_t*>(st), sm.ph.p1.cumul,
                                    sm.ph.p1.cnt,
-                                   [&](uint32_t i, uint32_t s, uint32_t r) {
-                                       st[cumul[s] + r] = (uint16_t)(size + i);  // fse.rs:157-162
+                                   [&](uint32_t i, uint32_t, uint32_t r) {
+                                       st[r] = (uint16_t)(size + i);  // fse.rs:157-162 (r = cumul[s] + rank)
                                    },
-                                   nullptr, reinterpret_cast<uint64_t*>(&sm.tt[b][0]));
+                                   [&](uint32_t s) { return (uint32_t)cumul[s]; }, nullptr,
+                                   reinterpret_cast<uint64_t*>(&sm.tt[b][0]));
             // symbol transforms, fse.rs:165-188 (total == cumul[s]), with
             // the stateTable's LDS address folded into deltaFindState
             const uint32_t stb = lds_addr_of(&sm.st[b][0]);
