@@ -14,6 +14,9 @@
 //
 // The table kernels run one wave on one item (the reference's per-call
 // granularity); the bitstream kernels are HBM-bound streaming passes.
+#include <atomic>
+#include <mutex>
+
 #include "fse_device.hpp"
 #include "fse_kernels.h"
 
@@ -126,7 +129,7 @@ __global__ __launch_bounds__(64) void hdr_read_kernel(const uint8_t* src, uint32
 // formulas (fse.rs:157-188, 329-337).
 // ------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void table_kernel(const fse_norm_histogram* nh, int enc, fse_encode_table* et, fse_decode_table* dt,
-                                                   int32_t* status) {
+                                                   int32_t* status, uint32_t peer_ranks) {
     constexpr uint32_t SMAX = 1u << LOG_MAX_REF;
     __shared__ __attribute__((aligned(16))) uint8_t sym_at[SMAX];
     __shared__ __attribute__((aligned(16))) uint8_t occ[SMAX];
@@ -150,7 +153,7 @@ __global__ __launch_bounds__(64) void table_kernel(const fse_norm_histogram* nh,
                 et->table[r] = (uint16_t)(size + i);  // fse.rs:157-162 (r = cumul[s] + rank)
                 et->symbols[i] = (uint8_t)s;
             },
-            [&](uint32_t s) { return (uint32_t)cumul[s]; });
+            [&](uint32_t s) { return (uint32_t)cumul[s]; }, peer_ranks == 0u);
         // symbol transforms (fse.rs:165-188); total before symbol s = cumul[s]
         for (uint32_t s = lane; s < 256u; s += WAVE) {
             uint32_t bits = 0;
@@ -185,7 +188,8 @@ __global__ __launch_bounds__(64) void table_kernel(const fse_norm_histogram* nh,
         [&](uint32_t s) {
             const int32_t v = norm[s];
             return v < 0 ? 1u : (uint32_t)v;
-        });
+        },
+        peer_ranks == 0u);
         uint32_t big = 0;  // fast_mode: no norm >= 2^(L-1) (fse.rs:302-305)
         for (uint32_t s = lane; s < tl; s += WAVE)
             if (norm[s] > 0 && (uint32_t)norm[s] >= (1u << (L - 1u))) big = 1;
@@ -419,8 +423,98 @@ hipError_t launch_hdr_read(const uint8_t* src, uint32_t n, fse_norm_histogram* o
 }
 hipError_t launch_table(const fse_norm_histogram* nh, int enc, fse_encode_table* et, fse_decode_table* dt, int32_t* status,
                         hipStream_t s) {
-    hipLaunchKernelGGL(table_kernel, dim3(1), dim3(64), 0, s, nh, enc, et, dt, status);
+    hipLaunchKernelGGL(table_kernel, dim3(1), dim3(64), 0, s, nh, enc, et, dt, status, rank_order_ok() ? 0u : 1u);
     return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------
+// The lane-order check behind the atomic ranks (wave_build_spread): every
+// lane of every wave draws a key (1..64 distinct keys, uniform or skewed)
+// and an activity bit, reads its key's LDS counter, does ds_add_rtn_u32 on
+// it, and compares the old value returned with counter-before + the active
+// lanes below it with the same key (ballot peers).  Counts the mismatches.
+// ------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t rc_mix(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+__global__ __launch_bounds__(256) void rank_order_check_kernel(uint32_t* bad, unsigned long long* total) {
+    __shared__ uint32_t cnt[4][64];
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    cnt[w][lane] = 0;
+    __syncthreads();
+    const uint32_t nkeys = 1u + (blockIdx.x % 64u), skew = (blockIdx.x >> 6) & 1u;
+    uint32_t nbad = 0, nops = 0;
+    for (uint32_t it = 0; it < 64u; ++it) {
+        const uint32_t h = rc_mix(it * 0x9E3779B9u ^ (blockIdx.x * 256u + threadIdx.x) * 0x85EBCA6Bu);
+        const uint32_t key = skew ? min((uint32_t)__builtin_ctz((h >> 8) | 0x80000000u), nkeys - 1u) : h % nkeys;
+        const bool act = (it & 1u) == 0u || ((h >> 5) & 7u) != 0u;  // every lane, then ~7/8 of them
+        const uint32_t before = cnt[w][key];
+        __builtin_amdgcn_wave_barrier();
+        uint32_t r = 0;
+        if (act)
+            r = __hip_atomic_fetch_add((__attribute__((address_space(3))) uint32_t*)&cnt[w][key], 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+        uint64_t peers = 0;
+        for (uint32_t k = 0; k < nkeys; ++k) {
+            const uint64_t m = __ballot(act && key == k);
+            if (key == k) peers = m;
+        }
+        const uint32_t below = (uint32_t)__popcll(peers & ((1ull << lane) - 1ull));
+        if (act) {
+            nops += 1u;
+            nbad += r != before + below ? 1u : 0u;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    atomicAdd(bad, nbad);
+    atomicAdd(total, (unsigned long long)nops);
+}
+
+hipError_t rank_order_check(uint32_t* violations, uint64_t* atomics) {
+    uint32_t* d = nullptr;
+    if (hipError_t e = hipMalloc(&d, 16)) return e;
+    hipError_t e = hipMemsetAsync(d, 0, 16, nullptr);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(rank_order_check_kernel, dim3(256), dim3(256), 0, nullptr, d,
+                           reinterpret_cast<unsigned long long*>(d + 2));
+        e = hipGetLastError();
+    }
+    uint32_t h[4] = {0, 0, 0, 0};
+    if (e == hipSuccess) e = hipMemcpy(h, d, 16, hipMemcpyDeviceToHost);  // waits for the kernel
+    (void)hipFree(d);
+    if (e != hipSuccess) return e;
+    *violations = h[0];
+    *atomics = (uint64_t)h[2] | ((uint64_t)h[3] << 32);
+    return hipSuccess;
+}
+
+static std::atomic<int> g_rank_mode{-1};  // fsehipx_rank_mode: -1 checked, 0 atomic, 1 peer-mask
+int rank_mode(int mode) { return g_rank_mode.exchange(mode); }
+
+bool rank_order_ok() {
+    const int forced = g_rank_mode.load(std::memory_order_relaxed);
+    if (forced >= 0) return forced == 0;
+    static std::atomic<int> state[64];  // per device: 0 unknown, 1 ok, 2 failed (or could not run)
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+    int st = state[dev].load(std::memory_order_acquire);
+    if (st == 0) {
+        static std::mutex mu;
+        std::lock_guard<std::mutex> g(mu);
+        st = state[dev].load(std::memory_order_relaxed);
+        if (st == 0) {
+            uint32_t v = 1;
+            uint64_t n = 0;
+            st = (rank_order_check(&v, &n) == hipSuccess && v == 0 && n > 0) ? 1 : 2;
+            state[dev].store(st, std::memory_order_release);
+        }
+    }
+    return st == 1;
 }
 
 hipError_t launch_host_return(const void* meta, const uint8_t* src, const uint32_t* len, void* hmeta, uint8_t* hdst,

@@ -1350,4 +1350,17 @@ int fsehipx_occupancy(char* buf, int cap) {
     return n < cap ? n + fsehip::occupancy_report_dec(buf + n, cap - n) : n;
 }
 
+// Diagnostics only: the lane-order check behind the table builds' atomic
+// ranks, run now (fse_kernels.h rank_order_check); FSE_OK with the counts.
+int fsehipx_rank_order_check(uint32_t* violations, uint64_t* atomics) {
+    if (!violations || !atomics) return FSE_ERR_BAD_ARG;
+    if (!device_ok()) return FSE_ERR_NO_DEVICE;
+    return fsehip::rank_order_check(violations, atomics) == hipSuccess ? FSE_OK : FSE_ERR_HIP;
+}
+
+// Diagnostics only: force the table builds' rank method (tests of the
+// fallback): -1 = the checked default, 0 = atomic ranks, 1 = peer-mask
+// ranks.  Returns the previous mode.
+int fsehipx_rank_mode(int mode) { return fsehip::rank_mode(mode < 0 ? -1 : mode > 0 ? 1 : 0); }
+
 }  // extern "C"

@@ -1021,8 +1021,11 @@ __global__ __launch_bounds__(64) void dtable_blocks_kernel(DtParams P) {
             return v < 0 ? 1u : (uint32_t)v;
         };
         // two-pass ranks need 2^L / 64 per-chunk registers: up to L = 12
-        if (LMAX <= 12) rc = wave_build_spread<SIZE / 64u>(norm, L, tl, sym_at, occ, cumul, cnt, visit, first_x, rk, pm, &P);
-        else rc = wave_build_spread(norm, L, tl, sym_at, occ, cumul, cnt, visit, first_x);
+        const bool atomic_ranks = P.peer_ranks == 0u;
+        if (LMAX <= 12)
+            rc = wave_build_spread<SIZE / 64u>(norm, L, tl, sym_at, occ, cumul, cnt, visit, first_x, atomic_ranks, rk, pm,
+                                               &P);
+        else rc = wave_build_spread(norm, L, tl, sym_at, occ, cumul, cnt, visit, first_x, atomic_ranks);
     }
     FSE_STAMP(P, 8);
     if (lane == 0) P.dtinfo[gb] = rc == FSE_OK ? (int32_t)((uint32_t)hl | (L << 16)) : rc;
@@ -2502,6 +2505,7 @@ int occupancy_report_dec(char* buf, int cap) {
 
 hipError_t launch_dtables(const DtParams& P0, uint32_t lmax, hipStream_t stream) {
     DtParams P = P0;
+    P.peer_ranks = rank_order_ok() ? 0u : 1u;
     if (lmax > 12) P.hdr_meta = nullptr;  // the staged rows hold headers up to L = 12
     if (P.hdr_meta && P.hdr_norm) {
         const dim3 gp((P.n_blocks + HP_BLOCKS - 1u) / HP_BLOCKS);

@@ -710,10 +710,12 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t v) { return dpp0<0x138, 0
 struct NoStamps {
     uint64_t* stamps = nullptr;
 };
+
 template <uint32_t MAXCH = 64, typename Visit, typename Base, class SP = NoStamps>  // MAXCH: 2^LMAX / 64 chunks (two-pass ranks)
 __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_t tl, uint8_t* sym_at,
                                         uint8_t* occ_sym, uint16_t* cumul, uint32_t* cnt, Visit visit, Base base,
-                                        uint16_t* RK = nullptr, uint64_t* PM = nullptr, const SP* SPp = nullptr) {
+                                        bool atomic_ranks, uint16_t* RK = nullptr, uint64_t* PM = nullptr,
+                                        const SP* SPp = nullptr) {
     // SPp: diagnostics only, a params struct with `stamps` (phase stamps 3..7)
 #define SPREAD_STAMP(k)                                  \
     do {                                                 \
@@ -816,6 +818,31 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
     }
     wave_sync();
     SPREAD_STAMP(5);
+    if (atomic_ranks) {
+    // Ranks by one LDS atomic per 64 positions: the old values that a
+    // ds_add_rtn_u32 hands to the lanes of one instruction hitting the same
+    // counter come in ascending lane order on gfx950 (tools/micro/
+    // lds_atomic_order.hip: 1.5e9 atomics, uniform and skewed keys, partial
+    // exec masks, none out of order), and the instructions run in position
+    // order, so the value is the count of s at earlier positions -- the
+    // rank -- on top of the caller's base.  The property is not documented:
+    // the library checks it once per device (rank_order_check_kernel,
+    // fsehip_rank_order_check) and passes atomic_ranks = false, the peer-mask
+    // ranks below, if it ever fails.
+    for (uint32_t s = lane; s < 256u; s += WAVE) cnt[s] = base(s);
+    wave_sync();
+    for (uint32_t i0 = 0; i0 < size; i0 += WAVE) {
+        const uint32_t i = i0 + lane;
+        if (i < size) {
+            const uint32_t sy = sym_at[i];
+            const uint32_t r = __hip_atomic_fetch_add((lds_u32*)cnt + sy, 1u, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+            visit(i, sy, r);
+        }
+    }
+    wave_sync();
+    return FSE_OK;
+    }
     if (RK != nullptr && tl <= 64u && size >= WAVE) {
         // pass 1: per 64-position chunk t, each symbol's count at RK[t][s]
         // (written by its lowest lane) and each lane's peers below, packed

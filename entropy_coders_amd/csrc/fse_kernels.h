@@ -28,6 +28,7 @@ struct EncParams {
                      // bit3 = histogram only, bit4 = no repair rounds
     uint64_t* stamps;  // diagnostics: per-workgroup s_memtime at phase ends
     uint32_t xlds;            // diagnostics: extra dynamic LDS bytes per workgroup (occupancy probe)
+    uint32_t peer_ranks;      // set by launch_encode: 1 = peer-mask ranks (rank_order_ok() failed)
 };
 
 struct DecParams {
@@ -79,6 +80,7 @@ struct DtParams {
     // diagnostics build only (FSEHIP_DT_PAR=1): with hdr_meta at L <= 11, the
     // 4-wave table kernel (dtable_par_kernel, a measured negative) instead
     uint32_t par;
+    uint32_t peer_ranks;  // set by launch_dtables: 1 = peer-mask ranks (rank_order_ok() failed)
 };
 constexpr uint64_t hdr_scratch_bytes(uint64_t n_blocks) { return n_blocks * (512u + 8u); }
 
@@ -109,6 +111,16 @@ hipError_t launch_hdr_read(const uint8_t* src, uint32_t n, fse_norm_histogram* o
                            hipStream_t s);
 hipError_t launch_table(const fse_norm_histogram* nh, int enc, fse_encode_table* et, fse_decode_table* dt,
                         int32_t* status, hipStream_t s);
+// The table builds rank positions with one LDS atomic per 64 positions,
+// which needs same-address ds_add_rtn_u32 results in ascending lane order
+// (fse_device.hpp wave_build_spread).  rank_order_check runs the check
+// kernel (synchronous; counts the violations among `atomics` checked);
+// rank_order_ok() runs it once per device and caches the answer (false on
+// any error), and the launchers fall back to peer-mask ranks when false.
+hipError_t rank_order_check(uint32_t* violations, uint64_t* atomics);
+bool rank_order_ok();
+// Tests: -1 = checked (default), 0 = atomic ranks, 1 = peer-mask ranks; returns the previous mode.
+int rank_mode(int mode);
 // Host-call return: the 16-byte record at meta and min(*len, max) bytes of
 // src into pinned host memory (hmeta, hdst; 16-byte aligned).
 hipError_t launch_host_return(const void* meta, const uint8_t* src, const uint32_t* len, void* hmeta, uint8_t* hdst,

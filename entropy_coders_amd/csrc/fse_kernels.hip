@@ -818,7 +818,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
                                    [&](uint32_t i, uint32_t, uint32_t r) {
                                        st[r] = (uint16_t)(size + i);  // fse.rs:157-162 (r = cumul[s] + rank)
                                    },
-                                   [&](uint32_t s) { return (uint32_t)cumul[s]; }, nullptr,
+                                   [&](uint32_t s) { return (uint32_t)cumul[s]; }, P.peer_ranks == 0u, nullptr,
                                    reinterpret_cast<uint64_t*>(&sm.tt[b][0]));
             // symbol transforms, fse.rs:165-188 (total == cumul[s]), with
             // the stateTable's LDS address folded into deltaFindState
@@ -1256,7 +1256,9 @@ __global__ __launch_bounds__(256) void generate_kernel(GenParams G) {
 #ifndef FSEHIP_ENC_WGS
 #define FSEHIP_ENC_WGS 11u  // resident encode workgroups per CU at L <= 11 (LDS-padded)
 #endif
-hipError_t launch_encode(const EncParams& P, uint32_t lmax, hipStream_t stream) {
+hipError_t launch_encode(const EncParams& P0, uint32_t lmax, hipStream_t stream) {
+    EncParams P = P0;
+    P.peer_ranks = rank_order_ok() ? 0u : 1u;
     // 32 lanes per block (two blocks per wave) for L <= 12 when asked for;
     // L 13..15 tables (64 KiB stateTable) run one block per workgroup
     const uint32_t T = (P.lanes == 32 && lmax <= 12) ? 32u : 64u;

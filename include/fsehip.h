@@ -352,7 +352,12 @@ int fsehip_compress_blocks(const fsehip_params* p, const uint8_t* d_src, uint64_
  *                  before the table build: batches of >= 256 blocks at
  *                  max_table_log <= 12, fsehip_build_dtables included;
  *                  without it the tables kernel parses on its own).
- * Growing a buffer synchronises the stream before freeing the old one. */
+ * Growing a buffer synchronises the stream before freeing the old one.
+ * First table build on a device (any encode or decode call): the library
+ * first runs a ~1 ms synchronous self-check on the null stream (the lane
+ * order of same-address LDS atomics that its rank pass relies on; the
+ * slower peer-mask ranks are used if it fails), so issue one call before
+ * capturing a stream into a graph. */
 int fsehip_decompress_blocks(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
                              const uint32_t* d_comp_len, const uint64_t* d_sidecar, uint8_t* d_out,
                              uint64_t n_total, int32_t* d_status, fsehip_stream_t stream);
