@@ -7,6 +7,7 @@ requires the property to hold here, so that the fast path is the one the
 other GPU tests exercise."""
 import ctypes as C
 
+import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -57,6 +58,11 @@ def test_peer_rank_fallback_matches_atomic(rank_mode, kind, prob, log2, nstates)
         nb = codec.n_blocks(n)
         lens = cb["comp_len"].cpu().numpy()
         blocks = cb["out"].view(nb, -1).cpu().numpy()
-        out[mode] = ([bytes(blocks[b, :lens[b]]) for b in range(nb)], cb["sidecar"].cpu().numpy().tobytes(),
-                     tabs["dt"].cpu().numpy().tobytes(), tabs["info"].cpu().numpy().tobytes())
+        info = tabs["info"].cpu().numpy()
+        per = int(codec.lib.fsehip_dtable_bytes(codec.max_table_log)) // 4
+        dt = tabs["dt"].cpu().numpy().view(np.uint32).reshape(nb, per)
+        assert (info >= 0).all()
+        tables = [dt[b, :1 << ((int(info[b]) >> 16) & 0xFF)].tobytes() for b in range(nb)]  # a table's 2^L entries
+        out[mode] = ([bytes(blocks[b, :lens[b]]) for b in range(nb)], cb["sidecar"].cpu().numpy().tobytes(), tables,
+                     info.tobytes())
     assert out[0] == out[1]
