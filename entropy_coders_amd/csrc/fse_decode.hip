@@ -588,7 +588,46 @@ struct PreSmem {
     uint32_t pay[PMAX / 4];
     uint32_t dt[1u << LMAX];
     int err[NW];
+    // in-workgroup table build (LMAX 11): rank counters (cumul aliased) and its status
+    uint32_t cnt[LMAX == 11 ? 256 : 1];
+    int brc;
 };
+
+// The block's decode table built in LDS by one wave (in-workgroup tables,
+// DecParams::hdr_meta): NormHistogram::read's counts from hdr_parse_kernel's
+// scratch, then DecodeTable (fse.rs:280-338) with the atomic ranks of
+// wave_build_spread straight into the staged-table region.  Scratch inside
+// that region: the occurrence owners at bytes [0, 2^11) (dead after the
+// spread walk, before any entry is written), the counts at [2^11, 2^11 +
+// 1 KiB) (last read when the rank counters start, before the entries of
+// positions >= 512 are written) and the symbol at each position at
+// [3 * 2^11, 4 * 2^11): entry i (bytes 4i..4i+3) overwrites only symbols of
+// positions <= i, already read by then.
+template <class Smem>
+__device__ __forceinline__ int inwg_build_table(const DecParams& P, Smem& sm, uint64_t gb, uint32_t L, uint32_t tl) {
+    constexpr uint32_t SIZE = 1u << 11;
+    const uint32_t lane = lane_id();
+    uint8_t* tb = reinterpret_cast<uint8_t*>(sm.dt);
+    int32_t* norm = reinterpret_cast<int32_t*>(tb + SIZE);
+    const uint32_t q0 = P.hdr_norm[gb * 128u + lane], q1 = P.hdr_norm[gb * 128u + 64u + lane];
+    norm[2u * lane] = (int32_t)(int16_t)(q0 & 0xFFFFu);
+    norm[2u * lane + 1u] = (int32_t)(int16_t)(q0 >> 16);
+    norm[128u + 2u * lane] = (int32_t)(int16_t)(q1 & 0xFFFFu);
+    norm[128u + 2u * lane + 1u] = (int32_t)(int16_t)(q1 >> 16);
+    wave_sync();
+    const uint32_t size = 1u << L;
+    uint32_t* dt = sm.dt;
+    auto visit = [&](uint32_t i, uint32_t s, uint32_t nx) {  // nx = the symbol's first x + rank
+        const uint32_t nb = L - ilog2u(nx);
+        dt[i] = Dte<11>::make(nb, s, (nx << nb) - size);
+    };
+    auto first_x = [&](uint32_t s) {  // symbol_next (fse.rs:296-308): 1 for a -1 count
+        const int32_t v = norm[s];
+        return v < 0 ? 1u : (uint32_t)v;
+    };
+    return wave_build_spread<SIZE / 64u>(norm, L, tl, tb + 3u * SIZE, tb, reinterpret_cast<uint16_t*>(sm.cnt), sm.cnt,
+                                         visit, first_x, true);
+}
 
 // One block (gb) by the whole workgroup; LDS reuse across calls is safe:
 // every reader of the image and table has passed the final barrier before
@@ -604,7 +643,24 @@ __device__ __forceinline__ void decode_pre_block(const DecParams& P, Smem& sm, c
     const uint64_t ooff = gb * (uint64_t)P.block_size;
     const uint32_t n = (uint32_t)min((uint64_t)P.block_size, P.n_total - ooff);
     uint8_t* out = P.out + ooff;
-    const int32_t info = P.dtinfo[gb];
+    // in-workgroup tables: the checks of dtable_blocks_kernel on the parsed header
+    constexpr bool INWG = LMAX == 11 && NS == 2;
+    const bool inwg = INWG && P.hdr_meta != nullptr;
+    int32_t info;
+    uint32_t tl = 0;
+    if (inwg) {
+        const int2 m = P.hdr_meta[gb];
+        int32_t hl = m.x;
+        if (hl >= 0) {
+            const uint32_t last = (clen && clen <= P.slot_bytes) ? in[clen - 1u] : 0u;
+            if ((uint32_t)hl >= clen || last == 0) hl = FSE_ERR_NO_MARKER;  // lib.rs:222
+            else if (clen > (1u << 28)) hl = FSE_ERR_UNSUPPORTED;
+        }
+        tl = (uint32_t)m.y >> 8;
+        info = hl < 0 ? hl : (int32_t)((uint32_t)hl | (((uint32_t)m.y & 0xFFu) << 16));
+    } else {
+        info = P.dtinfo[gb];
+    }
     const bool in_lds = !BIG && clen <= PMAX;
     if (P.pass >= 2 && P.status[gb] != FSE_DEFERRED) return;  // done by an earlier pass
     FSE_STAMP(P, 0);
@@ -619,22 +675,40 @@ __device__ __forceinline__ void decode_pre_block(const DecParams& P, Smem& sm, c
     const int32_t hdr_bits = (info & 0xFFFF) * 8;
     const uint32_t L = (uint32_t)info >> 16;
     {  // stage the block image and the table
-        if (in_lds && !(FSEHIP_ABL & 8)) {  // ABL 8 (timing only): decode whatever the LDS holds
+        // in-workgroup tables: wave 0 builds the table while the other waves
+        // stage the image (wave 0 issues no stage loads, so its waits on the
+        // header scratch do not wait on them)
+        const uint32_t w0 = inwg ? 1u : 0u;
+        if (in_lds && !(FSEHIP_ABL & 8) && wv >= w0) {  // ABL 8 (timing only): decode whatever the LDS holds
             const uint32_t nvec = (clen + 15u) >> 4;
             const uint4* src4 = reinterpret_cast<const uint4*>(in);
             uint4* dst4 = reinterpret_cast<uint4*>(sm.pay);
-            for (uint32_t i = wv * 64u; i < nvec; i += NT)
+            for (uint32_t i = (wv - w0) * 64u; i < nvec; i += NT - 64u * w0)
                 if (i + lane < nvec) __builtin_amdgcn_global_load_lds(src4 + i + lane, dst4 + i, 16, 0, FSEHIP_STAGE_AUX);
         }
-        const uint32_t dvec = 1u << L >> 2;  // 4 << L bytes
-        const uint4* t4 = reinterpret_cast<const uint4*>(P.dt + gb * (uint64_t)(1u << LMAX));
-        {
+        if (inwg) {
+            if constexpr (INWG) {
+                if (wv == 0) {
+                    const int rc = inwg_build_table(P, sm, gb, L, tl);
+                    if (lane == 0) sm.brc = rc;
+                }
+            }
+        } else {
+            const uint32_t dvec = 1u << L >> 2;  // 4 << L bytes
+            const uint4* t4 = reinterpret_cast<const uint4*>(P.dt + gb * (uint64_t)(1u << LMAX));
             uint4* d4 = reinterpret_cast<uint4*>(sm.dt);
             for (uint32_t i = wv * 64u; i < dvec; i += NT)
                 if (i + lane < dvec) __builtin_amdgcn_global_load_lds(t4 + i + lane, d4 + i, 16, 0, FSEHIP_STAGE_AUX);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        if (inwg && sm.brc != FSE_OK) {  // BAD_TABLE, as dtable_blocks_kernel reports it
+            if (tid == 0) {
+                P.status[gb] = sm.brc;
+                if (P.out_len) P.out_len[gb] = 0u;
+            }
+            return;
+        }
     }
     FSE_STAMP(P, 3);
 #if FSEHIP_ABL & 4  // ablation (timing only): stage, then stop
@@ -2371,7 +2445,9 @@ hipError_t launch_single(const DecParams& P, uint32_t lmax, hipStream_t stream) 
 // ------------------------------------------------------------------------
 hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) {
     const dim3 g(P.n_blocks);
-    if (!P.dt || !P.dtinfo) return hipErrorInvalidValue;
+    // in-workgroup tables: 2-state segment decode at L <= 11 only
+    const bool inwg = P.hdr_meta && P.hdr_norm;
+    if (inwg ? (!P.sidecar || P.nstates == 1 || lmax != 11) : (!P.dt || !P.dtinfo)) return hipErrorInvalidValue;
     if (!P.sidecar) {  // serial: sidecar-less blocks, reference-mode host streams, sidecar recording
         if (P.nstates == 1) {
             if (lmax <= 11 && P.states && P.bulk && !P.sidecar_out) {  // symbols deferred, as below
@@ -2501,6 +2577,14 @@ int occupancy_report_dec(char* buf, int cap) {
     one("serial_ring<11,8,2,defer>", reinterpret_cast<const void*>(serial_ring_kernel<11, 8, 2, true>), 128);
     one("sym_map<11>", reinterpret_cast<const void*>(sym_map_kernel<11>));
     return len;
+}
+
+hipError_t launch_hdr_parse(const DtParams& P, uint32_t lmax, hipStream_t stream) {
+    if (lmax > 12 || !P.hdr_meta || !P.hdr_norm) return hipErrorInvalidValue;
+    const dim3 gp((P.n_blocks + HP_BLOCKS - 1u) / HP_BLOCKS);
+    if (lmax <= 11) hipLaunchKernelGGL((hdr_parse_kernel<11>), gp, dim3(64), 0, stream, P);
+    else hipLaunchKernelGGL((hdr_parse_kernel<12>), gp, dim3(64), 0, stream, P);
+    return hipGetLastError();
 }
 
 hipError_t launch_dtables(const DtParams& P0, uint32_t lmax, hipStream_t stream) {
