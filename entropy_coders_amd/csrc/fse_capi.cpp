@@ -1398,8 +1398,11 @@ int fsehipx_rank_order_check(uint32_t* violations, uint64_t* atomics) {
 int fsehipx_rank_mode(int mode) { return fsehip::rank_mode(mode < 0 ? -1 : mode > 0 ? 1 : 0); }
 
 // Diagnostics only: 1 = fsehip_decompress_blocks builds the decode tables
-// inside the decode workgroups where it can (a measured negative, off by
-// default); returns the previous setting.
-int fsehipx_dec_inwg(int on) { return g_dec_inwg.exchange(on ? 1 : 0); }
+// inside the decode workgroups where it can (a measured negative; compiled
+// only with -DFSEHIP_DEC_INWG=1, else -1); returns the previous setting.
+#ifndef FSEHIP_DEC_INWG
+#define FSEHIP_DEC_INWG 0
+#endif
+int fsehipx_dec_inwg(int on) { return FSEHIP_DEC_INWG ? g_dec_inwg.exchange(on ? 1 : 0) : -1; }  // -1: not built in
 
 }  // extern "C"

@@ -588,11 +588,22 @@ struct PreSmem {
     uint32_t pay[PMAX / 4];
     uint32_t dt[1u << LMAX];
     int err[NW];
+#if FSEHIP_DEC_INWG
     // in-workgroup table build (LMAX 11): rank counters (cumul aliased) and its status
     uint32_t cnt[LMAX == 11 ? 256 : 1];
     int brc;
+#endif
 };
 
+// In-workgroup decode tables: compiled only with FSEHIP_DEC_INWG (a measured
+// negative, below).  Their 1 KiB of rank counters alone takes the 512-thread
+// segment kernel from 3 to 2 workgroups per CU (LDS is allocated in whole
+// granules: 3 x 54,324 B does not fit), which cost the product C2 decode
+// 11 % and C3 5-8 % even with the route switched off (profiles/r05/dec_inwg/).
+#ifndef FSEHIP_DEC_INWG
+#define FSEHIP_DEC_INWG 0
+#endif
+#if FSEHIP_DEC_INWG
 // The block's decode table built in LDS by one wave (in-workgroup tables,
 // DecParams::hdr_meta): NormHistogram::read's counts from hdr_parse_kernel's
 // scratch, then DecodeTable (fse.rs:280-338) with the atomic ranks of
@@ -628,6 +639,7 @@ __device__ __forceinline__ int inwg_build_table(const DecParams& P, Smem& sm, ui
     return wave_build_spread<SIZE / 64u>(norm, L, tl, tb + 3u * SIZE, tb, reinterpret_cast<uint16_t*>(sm.cnt), sm.cnt,
                                          visit, first_x, true);
 }
+#endif
 
 // One block (gb) by the whole workgroup; LDS reuse across calls is safe:
 // every reader of the image and table has passed the final barrier before
@@ -644,7 +656,7 @@ __device__ __forceinline__ void decode_pre_block(const DecParams& P, Smem& sm, c
     const uint32_t n = (uint32_t)min((uint64_t)P.block_size, P.n_total - ooff);
     uint8_t* out = P.out + ooff;
     // in-workgroup tables: the checks of dtable_blocks_kernel on the parsed header
-    constexpr bool INWG = LMAX == 11 && NS == 2;
+    constexpr bool INWG = FSEHIP_DEC_INWG && LMAX == 11 && NS == 2;
     const bool inwg = INWG && P.hdr_meta != nullptr;
     int32_t info;
     uint32_t tl = 0;
@@ -687,12 +699,14 @@ __device__ __forceinline__ void decode_pre_block(const DecParams& P, Smem& sm, c
                 if (i + lane < nvec) __builtin_amdgcn_global_load_lds(src4 + i + lane, dst4 + i, 16, 0, FSEHIP_STAGE_AUX);
         }
         if (inwg) {
+#if FSEHIP_DEC_INWG
             if constexpr (INWG) {
                 if (wv == 0) {
                     const int rc = inwg_build_table(P, sm, gb, L, tl);
                     if (lane == 0) sm.brc = rc;
                 }
             }
+#endif
         } else {
             const uint32_t dvec = 1u << L >> 2;  // 4 << L bytes
             const uint4* t4 = reinterpret_cast<const uint4*>(P.dt + gb * (uint64_t)(1u << LMAX));
@@ -702,6 +716,7 @@ __device__ __forceinline__ void decode_pre_block(const DecParams& P, Smem& sm, c
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+#if FSEHIP_DEC_INWG
         if (inwg && sm.brc != FSE_OK) {  // BAD_TABLE, as dtable_blocks_kernel reports it
             if (tid == 0) {
                 P.status[gb] = sm.brc;
@@ -709,6 +724,7 @@ __device__ __forceinline__ void decode_pre_block(const DecParams& P, Smem& sm, c
             }
             return;
         }
+#endif
     }
     FSE_STAMP(P, 3);
 #if FSEHIP_ABL & 4  // ablation (timing only): stage, then stop
@@ -2445,8 +2461,9 @@ hipError_t launch_single(const DecParams& P, uint32_t lmax, hipStream_t stream) 
 // ------------------------------------------------------------------------
 hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) {
     const dim3 g(P.n_blocks);
-    // in-workgroup tables: 2-state segment decode at L <= 11 only
+    // in-workgroup tables: 2-state segment decode at L <= 11 only (FSEHIP_DEC_INWG builds)
     const bool inwg = P.hdr_meta && P.hdr_norm;
+    if (inwg && !FSEHIP_DEC_INWG) return hipErrorInvalidValue;
     if (inwg ? (!P.sidecar || P.nstates == 1 || lmax != 11) : (!P.dt || !P.dtinfo)) return hipErrorInvalidValue;
     if (!P.sidecar) {  // serial: sidecar-less blocks, reference-mode host streams, sidecar recording
         if (P.nstates == 1) {
