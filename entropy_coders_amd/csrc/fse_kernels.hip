@@ -759,16 +759,40 @@ struct EncSmem {
     int scratch[4];
 };
 
+// Pooled-repair timing probe (variant builds only; DESIGN.md section 5,
+// encoder item 10): two blocks per 128-thread workgroup, one wave each, with
+// a workgroup barrier after the count passes and after the repair, where a
+// pooled repair (one wave repairing both blocks' lanes from a job queue)
+// would have them.  1: both waves repair their own block (the layout's
+// cost); 2: wave 1 skips its repair (wrong output) and waits at the barrier
+// while wave 0 repairs: the time a pool could reach with one repair wave
+// per two blocks doing one block's repair steps.
+#ifndef FSEHIP_ENC_POOLPROBE
+#define FSEHIP_ENC_POOLPROBE 0
+#endif
 template <int LMAX, int T, int NS>
-__global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
+constexpr int enc_nw() { return (FSEHIP_ENC_POOLPROBE && LMAX <= 11 && T == 64 && NS == 2) ? 2 : 1; }
+
+template <int LMAX, int T, int NS>
+__global__ __launch_bounds__((64 * enc_nw<LMAX, T, NS>())) void encode_blocks_kernel(EncParams P) {
     constexpr int BPW = 64 / T;
+#if FSEHIP_ENC_POOLPROBE
+    __shared__ EncSmem<LMAX, T> smv[enc_nw<LMAX, T, NS>()];
+    const uint32_t wv = enc_nw<LMAX, T, NS>() == 2 ? threadIdx.x >> 6 : 0u;
+    auto& sm = smv[wv];
+#define ENC_WGID ((uint64_t)blockIdx.x * enc_nw<LMAX, T, NS>() + wv)
+#define ENC_SYNC() wave_sync()
+#else
     __shared__ EncSmem<LMAX, T> sm;
+#define ENC_WGID ((uint64_t)blockIdx.x)
+#define ENC_SYNC() __syncthreads()
+#endif
     const uint32_t lane = lane_id();
 
     FSE_STAMP(P, 0);
     // ---- phase 1: statistics, header and tables, one block at a time
     for (int b = 0; b < BPW; ++b) {
-        const uint64_t gb = (uint64_t)blockIdx.x * BPW + b;
+        const uint64_t gb = ENC_WGID * BPW + b;
         if (gb >= P.n_blocks) {
             if (lane == 0) sm.info_status[b] = 1;  // no block
             continue;
@@ -872,7 +896,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
                 if (P.payload_bits) P.payload_bits[gb] = 0;
             }
         }
-        __syncthreads();
+        ENC_SYNC();
     }
 
     FSE_STAMP(P, 4);
@@ -880,7 +904,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     // ---- phase 2: T lanes per block
     const int b = BPW == 1 ? 0 : (int)(lane / T);
     const uint32_t k = BPW == 1 ? lane : lane % T;
-    const uint64_t gb = (uint64_t)blockIdx.x * BPW + b;
+    const uint64_t gb = ENC_WGID * BPW + b;
     const bool live = sm.info_status[b] == FSE_OK;
     const uint64_t boff = gb * P.block_size;
     const uint32_t n = live ? (uint32_t)min((uint64_t)P.block_size, P.n_total - boff) : 0u;
@@ -935,10 +959,16 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
             track_fixup(tr, nslot, -1, tot0, tot1);
         }
         FSE_STAMP(P, 5);
+#if FSEHIP_ENC_POOLPROBE
+        __syncthreads();  // a pool starts once both blocks' count passes are done
+#endif
         constexpr bool PC = NS == 2 && FSEHIP_ENC_PC && !(FSEHIP_ENC_ABL & 2);
         for (;;) {
             if (P.debug & 16u) break;  // ablation: no repair (wrong output)
-            __syncthreads();
+#if FSEHIP_ENC_POOLPROBE == 2
+            if (wv == 1u) break;
+#endif
+            ENC_SYNC();
             bool bad0 = false, bad1 = false;
             uint32_t nbF = 0;
             if (act && k < ktop) {
@@ -947,7 +977,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
                 bad1 = ((nbF ^ start) >> 16) != 0u;
             }
             const bool bad = bad0 || bad1;
-            __syncthreads();
+            ENC_SYNC();
             if (__ballot(bad) == 0) break;
             ++n_iter;
             n_rerun += (uint32_t)__popcll(__ballot(bad));
@@ -985,6 +1015,9 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
                 }
             }
         }
+#if FSEHIP_ENC_POOLPROBE
+        __syncthreads();  // ... and ends once both blocks are repaired
+#endif
         bits = tot0 + tot1;
         if (k == 0) bits += (uint32_t)NS * L + 1u;  // finals + marker (lib.rs:178-181 / 139-141)
     }
@@ -1009,7 +1042,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
 
     // emit pass (its ring overlays the trajectories and end states: every
     // lane is past the repair rounds here)
-    __syncthreads();
+    ENC_SYNC();
     if (act && fits) {
         em.start(gw, off, (P.debug & 4u) ? 0u : (uint32_t)(P.slot_bytes >> 2),  // debug bit 2: no payload stores (ablation)
                  &sm.ph.p2.ring[lane * RING_STRIDE]);
@@ -1048,11 +1081,11 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     }
     // boundary words -> merge list (entry order = stream order); the list
     // overlays the ring, so every lane's ring reads are done first
-    __syncthreads();
+    ENC_SYNC();
     for (uint32_t e = k; e < 2u * (T + 1u); e += T) {
         if (b < BPW) sm.ph.p2.mg.mword[b][e] = 0xFFFFFFFFu;
     }
-    __syncthreads();
+    ENC_SYNC();
     if (act && fits) {
         const uint32_t slot = 2u * (T - k);
         if ((off & 31u) != 0u && em.word > em.w0) {  // first word stored with the low bits empty
@@ -1071,7 +1104,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     }
     FSE_STAMP(P, 7);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stores above land before the merge rewrites
-    __syncthreads();
+    ENC_SYNC();
     // merge: each run of equal word indices is OR-ed by its first entry
     if (live && fits) {
         constexpr uint32_t NE = 2u * (T + 1u);
@@ -1111,6 +1144,9 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
         }
     }
 }
+
+#undef ENC_SYNC
+#undef ENC_WGID
 
 // ------------------------------------------------------------------------
 // Histogram::new per block (histogram::count), one wave per block.
@@ -1284,6 +1320,12 @@ hipError_t launch_encode(const EncParams& P0, uint32_t lmax, hipStream_t stream)
             const size_t per = (160u << 10) / FSEHIP_ENC_WGS - 64u;  // LDS per workgroup for 11, less allocation slack
             return fa.sharedSizeBytes < per ? (uint32_t)(per - fa.sharedSizeBytes) : 0u;
         }();
+#if FSEHIP_ENC_POOLPROBE
+        if (lmax <= 11) {
+            hipLaunchKernelGGL((encode_blocks_kernel<11, 64, 2>), dim3((P.n_blocks + 1u) / 2u), dim3(128), 0, stream, P);
+            return hipGetLastError();
+        }
+#endif
         if (lmax <= 11) go(encode_blocks_kernel<11, 64, 2>, pad11);
         else if (lmax <= 12) go(encode_blocks_kernel<12, 64, 2>);
         else if (lmax <= 13) go(encode_blocks_kernel<13, 64, 2>);
