@@ -462,7 +462,6 @@ static void defer_symbols(Lease& lease, fsehip::DecParams& P, uint32_t lmax) {
     P.states = P.bulk ? static_cast<uint32_t*>(lease.get(SCRATCH_STATES, 2ull * P.n_blocks * P.block_size, true))
                       : nullptr;
     if (!P.states || !P.bulk) P.states = P.bulk = nullptr;
-    if (env_u32("FSEHIP_SERIAL_DW", 1) == 2) P.pass = 7u;  // diagnostics: two decode waves (launch_decode)
 }
 
 // Decode on prebuilt tables (dtable_blocks_kernel at stride kern_lmax):
@@ -472,10 +471,8 @@ static int decompress_impl(const fsehip_params* p, const uint8_t* d_in, uint64_t
                            const uint32_t* d_comp_len, const uint64_t* d_sidecar, uint8_t* d_out, uint64_t n_total,
                            uint64_t* d_sidecar_out, int32_t* d_status, uint32_t* d_out_len, uint32_t out_cap,
                            fsehip_stream_t stream, const uint32_t* d_dt, const int32_t* d_dtinfo,
-                           Lease* lease = nullptr, const int2* d_hdr_meta = nullptr,
-                           const uint32_t* d_hdr_norm = nullptr) {
-    const bool inwg = d_hdr_meta && d_hdr_norm;  // tables built in the decode workgroups (DecParams::hdr_meta)
-    if (!p || !d_in || !d_comp_len || !d_out || !d_status || (!inwg && (!d_dt || !d_dtinfo))) return FSE_ERR_BAD_ARG;
+                           Lease* lease = nullptr) {
+    if (!p || !d_in || !d_comp_len || !d_out || !d_status || !d_dt || !d_dtinfo) return FSE_ERR_BAD_ARG;
     const uint32_t bs = p->block_size ? p->block_size : kDefaultBlock;
     if (bs > kMaxBlock) return FSE_ERR_UNSUPPORTED;
     const uint64_t n_blocks = n_total ? (n_total + bs - 1) / bs : 1;
@@ -511,10 +508,6 @@ static int decompress_impl(const fsehip_params* p, const uint8_t* d_in, uint64_t
     P.sidecar_out = d_sidecar_out;
     P.dt = d_dt;
     P.dtinfo = d_dtinfo;
-    if (inwg) {
-        P.hdr_meta = d_hdr_meta;
-        P.hdr_norm = d_hdr_norm;
-    }
     if (lease && !d_sidecar && !d_sidecar_out) defer_symbols(*lease, P, kern_lmax(p->max_table_log));
     P.stamps = g_stamps_dec.get(n_blocks);
     hipError_t e = fsehip::launch_decode(P, kern_lmax(p->max_table_log), static_cast<hipStream_t>(stream));
@@ -548,7 +541,6 @@ static int build_dtables_impl(const fsehip_params* p, const uint8_t* d_in, uint6
     D.dt = d_dtables;
     D.dtinfo = d_dtinfo;
     D.xlds = env_u32("FSEHIP_DT_XLDS", 0);  // diagnostics: occupancy probe
-    D.par = env_u32("FSEHIP_DT_PAR", 0);  // diagnostics: the 4-wave table kernel (A/B)
     D.stamps = g_stamps_dt.get(n_blocks);
     hipError_t e = fsehip::launch_dtables(D, kern_lmax(p->max_table_log), static_cast<hipStream_t>(stream));
     if (D.stamps) g_stamps_dt.report("dtables", n_blocks, static_cast<hipStream_t>(stream));
@@ -603,40 +595,12 @@ static int with_dtables(const fsehip_params* p, const uint8_t* d_in, uint64_t sl
 }
 }  // extern "C++"
 
-static std::atomic<int> g_dec_inwg{0};  // fsehipx_dec_inwg
-
 int fsehip_decompress_blocks(const fsehip_params* p, const uint8_t* d_in, uint64_t slot_bytes,
                              const uint32_t* d_comp_len, const uint64_t* d_sidecar, uint8_t* d_out, uint64_t n_total,
                              int32_t* d_status, fsehip_stream_t stream) {
     if (n_total == 0) return FSE_ERR_EMPTY;
     if (!p) return FSE_ERR_BAD_ARG;
     if (d_sidecar && p->ckpt_interval == 0) return FSE_ERR_BAD_ARG;
-    // Off by default (fsehipx_dec_inwg): segment decode of 2-state blocks at
-    // table log <= 11 with the headers parsed one per lane into the stream's
-    // header scratch and each decode workgroup building its block's table in
-    // LDS while its image is staged (no table kernel, no table round trip
-    // through HBM).  Exact, but measured slower (C2 decode 0.69 against 0.55
-    // ms, profiles/r05/dec_inwg/): one wave's build outlasts the stage.
-    const uint32_t bs = p->block_size ? p->block_size : kDefaultBlock;
-    const uint64_t nb = bs <= kMaxBlock ? (n_total + bs - 1) / bs : 0;
-    if (g_dec_inwg.load(std::memory_order_relaxed) && d_sidecar && p->nstates != 1 &&
-        kern_lmax(p->max_table_log) == 11 && nb >= 256u && nb <= 0xFFFFFFFFull && d_in && d_comp_len &&
-        !(slot_bytes & 255u) && device_ok() && fsehip::rank_order_ok()) {
-        Lease lease(stream);
-        uint8_t* h = static_cast<uint8_t*>(lease.get(SCRATCH_HDR, fsehip::hdr_scratch_bytes(nb), true));
-        if (h) {
-            fsehip::DtParams D{};
-            D.in = d_in;
-            D.slot_bytes = slot_bytes;
-            D.comp_len = d_comp_len;
-            D.n_blocks = (uint32_t)nb;
-            D.hdr_norm = reinterpret_cast<uint32_t*>(h);
-            D.hdr_meta = reinterpret_cast<int2*>(h + 512ull * nb);
-            if (fsehip::launch_hdr_parse(D, 11, static_cast<hipStream_t>(stream)) != hipSuccess) return FSE_ERR_HIP;
-            return decompress_impl(p, d_in, slot_bytes, d_comp_len, d_sidecar, d_out, n_total, nullptr, d_status,
-                                   nullptr, 0, stream, nullptr, nullptr, &lease, D.hdr_meta, D.hdr_norm);
-        }
-    }
     return with_dtables(p, d_in, slot_bytes, d_comp_len, n_total, stream,
                         [&](const uint32_t* dt, const int32_t* info, Lease& lease) {
                             return decompress_impl(p, d_in, slot_bytes, d_comp_len, d_sidecar, d_out, n_total, nullptr,
@@ -1396,13 +1360,5 @@ int fsehipx_rank_order_check(uint32_t* violations, uint64_t* atomics) {
 // fallback): -1 = the checked default, 0 = atomic ranks, 1 = peer-mask
 // ranks.  Returns the previous mode.
 int fsehipx_rank_mode(int mode) { return fsehip::rank_mode(mode < 0 ? -1 : mode > 0 ? 1 : 0); }
-
-// Diagnostics only: 1 = fsehip_decompress_blocks builds the decode tables
-// inside the decode workgroups where it can (a measured negative; compiled
-// only with -DFSEHIP_DEC_INWG=1, else -1); returns the previous setting.
-#ifndef FSEHIP_DEC_INWG
-#define FSEHIP_DEC_INWG 0
-#endif
-int fsehipx_dec_inwg(int on) { return FSEHIP_DEC_INWG ? g_dec_inwg.exchange(on ? 1 : 0) : -1; }  // -1: not built in
 
 }  // extern "C"

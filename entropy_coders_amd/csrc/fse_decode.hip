@@ -26,21 +26,12 @@
 #include "fse_device.hpp"
 #include "fse_kernels.h"
 
-// FSEHIP_ABL: decode ablations for A/B timing builds only
-// (tools/variant_build.sh); the product is built with 0.
-#ifndef FSEHIP_ABL
-#define FSEHIP_ABL 0
-#endif
-// cache policy of the segment decoder's LDS-DMA staging loads: nt (2), as the image and table
-// are read once (C3 0.96 -> 0.91-0.96 ms, C2 decode 0.558 -> 0.552-0.554 ms, same box)
-#ifndef FSEHIP_DEC1_TX  // 1-state segments through the transposed group stores
-#define FSEHIP_DEC1_TX 1
-#endif
-#ifndef FSEHIP_STAGE_AUX
-#define FSEHIP_STAGE_AUX 2
-#endif
 
 namespace fsehip {
+
+// cache policy of the segment decoder's LDS-DMA staging loads: nt (2), as the image and table
+// are read once (C3 0.96 -> 0.91-0.96 ms, C2 decode 0.558 -> 0.552-0.554 ms, same box)
+constexpr int STAGE_AUX = 2;
 
 // ------------------------------------------------------------------------
 // Decode table entry (fse.rs:260-265 DecodeTransform, repacked for the
@@ -234,24 +225,9 @@ struct LdsChain {
     }
     __device__ __forceinline__ uint32_t pair(const uint32_t* pay, const uint8_t* dtb) {
         const int32_t lo = (pos - PAIR_MAX_BITS) & ~31;
-#if FSEHIP_ABL & 1  // ablation (timing only, wrong output): conflict-free payload reads
-        const int32_t wabl = max(((lo >> 5) & ~31) + (int32_t)(__builtin_amdgcn_workitem_id_x() & 31u), 0);
-        const uint32_t w0 = pay[wabl];
-#elif FSEHIP_ABL & 10  // garbage states may run a segment below the image: stay inside it
-        const uint32_t w0 = pay[max(lo >> 5, -1)];
-#elif FSEHIP_ABL & 1024  // upper bound (timing only, wrong output): no payload LDS read at all, the word from registers
-        const uint32_t w0 = (whi * 0x9E3779B1u) ^ (uint32_t)lo;
-#else
         const uint32_t w0 = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(pay) + (lo >> 3));
-#endif
-#if FSEHIP_ABL & 2  // ablation (timing only, wrong output): conflict-free table reads
-        const uint32_t lb = (__builtin_amdgcn_workitem_id_x() & 31u) << 2;
-        const uint32_t e0 = *reinterpret_cast<const uint32_t*>(dtb + ((a0 & ~0x7Fu) | lb));
-        const uint32_t e1 = *reinterpret_cast<const uint32_t*>(dtb + ((a1 & ~0x7Fu) | lb));
-#else
         const uint32_t e0 = *reinterpret_cast<const uint32_t*>(dtb + a0);
         const uint32_t e1 = *reinterpret_cast<const uint32_t*>(dtb + a1);
-#endif
         const uint32_t w1 = lo == B ? whi : wlo;
         pos -= (int32_t)((e0 + e1) & 0xFFu);
         const uint32_t x = (uint32_t)((((uint64_t)w1 << 32) | w0) >> (uint32_t)(pos - lo));
@@ -262,64 +238,7 @@ struct LdsChain {
         const uint32_t v0 = __builtin_amdgcn_ubfe(x, e1, e0);
         a0 = (e0 >> 16) + (v0 << 2);
         a1 = (e1 >> 16) + (v1 << 2);
-#if FSEHIP_ABL & 64  // A/B (timing only): 4 extra independent VALU per pair
-        {
-            uint32_t d0 = e0 ^ 0x1234u, d1 = e1 + 77u, d2 = x * 3u, d3 = w0 | 5u;
-            asm volatile("; pad %0 %1 %2 %3" ::"v"(d0), "v"(d1), "v"(d2), "v"(d3));
-        }
-#endif
-#if FSEHIP_ABL & 256  // sensitivity probe (timing only): one more random table-like LDS read per pair
-        {
-            const uint32_t dx = *reinterpret_cast<const uint32_t*>(dtb + (((a1 ^ (a0 << 7)) * 0x9E3779B1u >> 19) & 0x1FFCu));
-            asm volatile("; sink %0" ::"v"(dx));
-        }
-#endif
-#if FSEHIP_ABL & 512  // sensitivity probe (timing only): one more payload-like LDS read per pair (the word below)
-        {
-            const uint32_t dx = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(pay) + (lo >> 3) - 4);
-            asm volatile("; sink %0" ::"v"(dx));
-        }
-#endif
         return __builtin_amdgcn_perm(e1, e0, 0x0c0c0501u);  // sym0 | sym1 << 8
-    }
-    // Two pairs with one payload read: a pair takes <= 28 bits, so the
-    // second pair's window base is the first's (lo) or one word below it, and
-    // one ds_read2_b32 of words lo/32 - 1 and lo/32 serves both (the 16-byte
-    // pad below the image covers word -2).  One LDS instruction fewer per two
-    // pairs, and the second pair's address arithmetic is a select.
-    __device__ __forceinline__ void pair2(const uint32_t* pay, const uint8_t* dtb, uint32_t& ra, uint32_t& rb) {
-        const int32_t loA = (pos - PAIR_MAX_BITS) & ~31;
-        const uint32_t* wp = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(pay) + (loA >> 3) - 4);
-        const uint32_t q1 = wp[0], q0 = wp[1];  // words lo/32 - 1, lo/32
-        {
-            const uint32_t e0 = *reinterpret_cast<const uint32_t*>(dtb + a0);
-            const uint32_t e1 = *reinterpret_cast<const uint32_t*>(dtb + a1);
-            const uint32_t w1 = loA == B ? whi : wlo;
-            pos -= (int32_t)((e0 + e1) & 0xFFu);
-            const uint32_t x = (uint32_t)((((uint64_t)w1 << 32) | q0) >> (uint32_t)(pos - loA));
-            B = loA;
-            whi = w1;
-            wlo = q0;
-            a0 = (e0 >> 16) + (__builtin_amdgcn_ubfe(x, e1, e0) << 2);
-            a1 = (e1 >> 16) + (__builtin_amdgcn_ubfe(x, 0u, e1) << 2);
-            ra = __builtin_amdgcn_perm(e1, e0, 0x0c0c0501u);
-        }
-        {
-            const int32_t loB = (pos - PAIR_MAX_BITS) & ~31;  // loA or loA - 32
-            const uint32_t e0 = *reinterpret_cast<const uint32_t*>(dtb + a0);
-            const uint32_t e1 = *reinterpret_cast<const uint32_t*>(dtb + a1);
-            const bool same = loB == loA;
-            const uint32_t w1 = same ? whi : wlo;
-            const uint32_t w0 = same ? q0 : q1;
-            pos -= (int32_t)((e0 + e1) & 0xFFu);
-            const uint32_t x = (uint32_t)((((uint64_t)w1 << 32) | w0) >> (uint32_t)(pos - loB));
-            B = loB;
-            whi = w1;
-            wlo = w0;
-            a0 = (e0 >> 16) + (__builtin_amdgcn_ubfe(x, e1, e0) << 2);
-            a1 = (e1 >> 16) + (__builtin_amdgcn_ubfe(x, 0u, e1) << 2);
-            rb = __builtin_amdgcn_perm(e1, e0, 0x0c0c0501u);
-        }
     }
     __device__ __forceinline__ uint32_t s0() const { return a0 >> 2; }
     __device__ __forceinline__ uint32_t s1() const { return a1 >> 2; }
@@ -328,31 +247,13 @@ struct LdsChain {
         return *reinterpret_cast<const uint32_t*>(dtb + 4u * s);
     }
 };
-// pair2 in the group loops (A/B knob; the FSEHIP_ABL probes live in pair()).
-// Measured no faster (profiles/r05/dec_pair2/): C3 0.875-0.922 against
-// 0.885-0.918 ms, C2 decode 0.509-0.522 against 0.505-0.511, same box, exact
-// -- unlike the encoder, one LDS instruction fewer per two pairs (and half a
-// VALU op more) does not move the decoder.  Off by default.
-#ifndef FSEHIP_DEC_PAIR2
-#define FSEHIP_DEC_PAIR2 0
-#endif
+// Two pairs -> four output bytes (lo.b0 lo.b1 hi.b0 hi.b1).
 template <class Chain, class Tab>
 __device__ __forceinline__ uint32_t two_pairs(Chain& c, const uint32_t* pay, const Tab& dtb) {
     const uint32_t lo = c.pair(pay, dtb);
     const uint32_t hi = c.pair(pay, dtb);
     return __builtin_amdgcn_perm(hi, lo, 0x05040100u);  // lo.b0 lo.b1 hi.b0 hi.b1
 }
-__device__ __forceinline__ uint32_t two_pairs(LdsChain& c, const uint32_t* pay, const uint8_t* const& dtb) {
-#if FSEHIP_DEC_PAIR2 && !FSEHIP_ABL
-    uint32_t lo, hi;
-    c.pair2(pay, dtb, lo, hi);
-#else
-    const uint32_t lo = c.pair(pay, dtb);
-    const uint32_t hi = c.pair(pay, dtb);
-#endif
-    return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
-}
-
 // Bits [pos, pos + 32) of an LDS-staged block (pos >= 0): one ds_read2 of
 // the two words holding them and a v_alignbit (the end-of-block steps).
 __device__ __forceinline__ uint32_t lds_bits32(const uint32_t* pay, int32_t pos) {
@@ -363,16 +264,9 @@ __device__ __forceinline__ uint32_t lds_bits32(const uint32_t* pay, int32_t pos)
 // 32 pairs = one whole 64-byte piece of output per lane, stored back to
 // back (full HBM write bursts instead of masked partial ones).
 __device__ __forceinline__ void store_group(uint8_t* __restrict__ dst, const uint32_t* w) {
-#if FSEHIP_ABL & 16  // ablation (timing only): no output stores, the values kept live
-#pragma unroll
-    for (uint32_t q = 0; q < DEC_GROUP / 8u; ++q)
-        asm volatile("; sink %0 %1 %2 %3" ::"v"(w[4 * q]), "v"(w[4 * q + 1]), "v"(w[4 * q + 2]), "v"(w[4 * q + 3]));
-    (void)dst;
-#else
     uint4* o4 = reinterpret_cast<uint4*>(dst);
 #pragma unroll
     for (uint32_t q = 0; q < DEC_GROUP / 8u; ++q) o4[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
-#endif
 }
 
 // Output pieces through the wave's rows.  Lane (row r, column i) = lane
@@ -419,14 +313,6 @@ __device__ __forceinline__ void run_groups_tx(Chain& c, uint32_t my_ng, uint32_t
             for (uint32_t j = 0; j < DEC_GROUP / 2u; ++j) w[j] = 0;
         }
         rows_transpose(w);
-#if FSEHIP_ABL & 16  // ablation (timing only): no output stores, the values kept live
-        (void)obase;
-        (void)ong;
-        (void)row;
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            asm volatile("; sink %0 %1 %2 %3" ::"v"(w[4 * k]), "v"(w[4 * k + 1]), "v"(w[4 * k + 2]), "v"(w[4 * k + 3]));
-#else
         // non-temporal: the output is written once and not read back here, so
         // it should not displace the images, tables and sidecars in L2
         // (C3 0.95 -> 0.91 ms, C2 decode 0.60 -> 0.57 ms, same box)
@@ -435,7 +321,6 @@ __device__ __forceinline__ void run_groups_tx(Chain& c, uint32_t my_ng, uint32_t
             if (g < ong[k])
                 __builtin_nontemporal_store(u32x4{w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]},
                                             reinterpret_cast<u32x4*>(obase[k] + g * 2u * DEC_GROUP + 16u * row));
-#endif
     }
 }
 
@@ -572,74 +457,16 @@ __device__ __forceinline__ int32_t run_chain1(LdsChain1& c, const uint32_t* pay,
 // Segment of thread tid in a round of 256.
 template <uint32_t NT = 256u>
 __device__ __forceinline__ uint32_t seg_of(uint32_t tid) {
-#if FSEHIP_ABL & 32  // A/B: consecutive segments on consecutive lanes
-    return tid;
-#else
     return (tid * 33u) & (NT - 1u);  // a bijection of [0, NT): 33 is odd
-#endif
 }
 
 template <int LMAX, uint32_t PMAX, uint32_t NW = 4u>
 struct PreSmem {
-#if FSEHIP_ABL & 128  // A/B (timing only): 30 KiB more LDS, 2 workgroups per CU
-    uint32_t occ_pad[(30u << 10) / 4];
-#endif
     uint32_t pad[4];  // below the image: the window may start at word -1
     uint32_t pay[PMAX / 4];
     uint32_t dt[1u << LMAX];
     int err[NW];
-#if FSEHIP_DEC_INWG
-    // in-workgroup table build (LMAX 11): rank counters (cumul aliased) and its status
-    uint32_t cnt[LMAX == 11 ? 256 : 1];
-    int brc;
-#endif
 };
-
-// In-workgroup decode tables: compiled only with FSEHIP_DEC_INWG (a measured
-// negative, below).  Their 1 KiB of rank counters alone takes the 512-thread
-// segment kernel from 3 to 2 workgroups per CU (LDS is allocated in whole
-// granules: 3 x 54,324 B does not fit), which cost the product C2 decode
-// 11 % and C3 5-8 % even with the route switched off (profiles/r05/dec_inwg/).
-#ifndef FSEHIP_DEC_INWG
-#define FSEHIP_DEC_INWG 0
-#endif
-#if FSEHIP_DEC_INWG
-// The block's decode table built in LDS by one wave (in-workgroup tables,
-// DecParams::hdr_meta): NormHistogram::read's counts from hdr_parse_kernel's
-// scratch, then DecodeTable (fse.rs:280-338) with the atomic ranks of
-// wave_build_spread straight into the staged-table region.  Scratch inside
-// that region: the occurrence owners at bytes [0, 2^11) (dead after the
-// spread walk, before any entry is written), the counts at [2^11, 2^11 +
-// 1 KiB) (last read when the rank counters start, before the entries of
-// positions >= 512 are written) and the symbol at each position at
-// [3 * 2^11, 4 * 2^11): entry i (bytes 4i..4i+3) overwrites only symbols of
-// positions <= i, already read by then.
-template <class Smem>
-__device__ __forceinline__ int inwg_build_table(const DecParams& P, Smem& sm, uint64_t gb, uint32_t L, uint32_t tl) {
-    constexpr uint32_t SIZE = 1u << 11;
-    const uint32_t lane = lane_id();
-    uint8_t* tb = reinterpret_cast<uint8_t*>(sm.dt);
-    int32_t* norm = reinterpret_cast<int32_t*>(tb + SIZE);
-    const uint32_t q0 = P.hdr_norm[gb * 128u + lane], q1 = P.hdr_norm[gb * 128u + 64u + lane];
-    norm[2u * lane] = (int32_t)(int16_t)(q0 & 0xFFFFu);
-    norm[2u * lane + 1u] = (int32_t)(int16_t)(q0 >> 16);
-    norm[128u + 2u * lane] = (int32_t)(int16_t)(q1 & 0xFFFFu);
-    norm[128u + 2u * lane + 1u] = (int32_t)(int16_t)(q1 >> 16);
-    wave_sync();
-    const uint32_t size = 1u << L;
-    uint32_t* dt = sm.dt;
-    auto visit = [&](uint32_t i, uint32_t s, uint32_t nx) {  // nx = the symbol's first x + rank
-        const uint32_t nb = L - ilog2u(nx);
-        dt[i] = Dte<11>::make(nb, s, (nx << nb) - size);
-    };
-    auto first_x = [&](uint32_t s) {  // symbol_next (fse.rs:296-308): 1 for a -1 count
-        const int32_t v = norm[s];
-        return v < 0 ? 1u : (uint32_t)v;
-    };
-    return wave_build_spread<SIZE / 64u>(norm, L, tl, tb + 3u * SIZE, tb, reinterpret_cast<uint16_t*>(sm.cnt), sm.cnt,
-                                         visit, first_x, true);
-}
-#endif
 
 // One block (gb) by the whole workgroup; LDS reuse across calls is safe:
 // every reader of the image and table has passed the final barrier before
@@ -655,24 +482,7 @@ __device__ __forceinline__ void decode_pre_block(const DecParams& P, Smem& sm, c
     const uint64_t ooff = gb * (uint64_t)P.block_size;
     const uint32_t n = (uint32_t)min((uint64_t)P.block_size, P.n_total - ooff);
     uint8_t* out = P.out + ooff;
-    // in-workgroup tables: the checks of dtable_blocks_kernel on the parsed header
-    constexpr bool INWG = FSEHIP_DEC_INWG && LMAX == 11 && NS == 2;
-    const bool inwg = INWG && P.hdr_meta != nullptr;
-    int32_t info;
-    uint32_t tl = 0;
-    if (inwg) {
-        const int2 m = P.hdr_meta[gb];
-        int32_t hl = m.x;
-        if (hl >= 0) {
-            const uint32_t last = (clen && clen <= P.slot_bytes) ? in[clen - 1u] : 0u;
-            if ((uint32_t)hl >= clen || last == 0) hl = FSE_ERR_NO_MARKER;  // lib.rs:222
-            else if (clen > (1u << 28)) hl = FSE_ERR_UNSUPPORTED;
-        }
-        tl = (uint32_t)m.y >> 8;
-        info = hl < 0 ? hl : (int32_t)((uint32_t)hl | (((uint32_t)m.y & 0xFFu) << 16));
-    } else {
-        info = P.dtinfo[gb];
-    }
+    const int32_t info = P.dtinfo[gb];
     const bool in_lds = !BIG && clen <= PMAX;
     if (P.pass >= 2 && P.status[gb] != FSE_DEFERRED) return;  // done by an earlier pass
     FSE_STAMP(P, 0);
@@ -687,50 +497,24 @@ __device__ __forceinline__ void decode_pre_block(const DecParams& P, Smem& sm, c
     const int32_t hdr_bits = (info & 0xFFFF) * 8;
     const uint32_t L = (uint32_t)info >> 16;
     {  // stage the block image and the table
-        // in-workgroup tables: wave 0 builds the table while the other waves
-        // stage the image (wave 0 issues no stage loads, so its waits on the
-        // header scratch do not wait on them)
-        const uint32_t w0 = inwg ? 1u : 0u;
-        if (in_lds && !(FSEHIP_ABL & 8) && wv >= w0) {  // ABL 8 (timing only): decode whatever the LDS holds
+        if (in_lds) {
             const uint32_t nvec = (clen + 15u) >> 4;
             const uint4* src4 = reinterpret_cast<const uint4*>(in);
             uint4* dst4 = reinterpret_cast<uint4*>(sm.pay);
-            for (uint32_t i = (wv - w0) * 64u; i < nvec; i += NT - 64u * w0)
-                if (i + lane < nvec) __builtin_amdgcn_global_load_lds(src4 + i + lane, dst4 + i, 16, 0, FSEHIP_STAGE_AUX);
+            for (uint32_t i = wv * 64u; i < nvec; i += NT)
+                if (i + lane < nvec) __builtin_amdgcn_global_load_lds(src4 + i + lane, dst4 + i, 16, 0, STAGE_AUX);
         }
-        if (inwg) {
-#if FSEHIP_DEC_INWG
-            if constexpr (INWG) {
-                if (wv == 0) {
-                    const int rc = inwg_build_table(P, sm, gb, L, tl);
-                    if (lane == 0) sm.brc = rc;
-                }
-            }
-#endif
-        } else {
+        {
             const uint32_t dvec = 1u << L >> 2;  // 4 << L bytes
             const uint4* t4 = reinterpret_cast<const uint4*>(P.dt + gb * (uint64_t)(1u << LMAX));
             uint4* d4 = reinterpret_cast<uint4*>(sm.dt);
             for (uint32_t i = wv * 64u; i < dvec; i += NT)
-                if (i + lane < dvec) __builtin_amdgcn_global_load_lds(t4 + i + lane, d4 + i, 16, 0, FSEHIP_STAGE_AUX);
+                if (i + lane < dvec) __builtin_amdgcn_global_load_lds(t4 + i + lane, d4 + i, 16, 0, STAGE_AUX);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-#if FSEHIP_DEC_INWG
-        if (inwg && sm.brc != FSE_OK) {  // BAD_TABLE, as dtable_blocks_kernel reports it
-            if (tid == 0) {
-                P.status[gb] = sm.brc;
-                if (P.out_len) P.out_len[gb] = 0u;
-            }
-            return;
-        }
-#endif
     }
     FSE_STAMP(P, 3);
-#if FSEHIP_ABL & 4  // ablation (timing only): stage, then stop
-    if (tid == 0) P.status[gb] = FSE_OK;
-    return;
-#endif
     const uint32_t smask = (1u << L) - 1u;
     // main-loop steps: pairs (NS = 2) or symbols below the last one (NS = 1)
     const uint32_t Pm = NS == 2 ? ((n & 1u) ? (n - 3u) / 2u : n / 2u - 1u) : n - 1u;
@@ -831,7 +615,7 @@ __device__ __forceinline__ void decode_pre_block(const DecParams& P, Smem& sm, c
             if (r != FSE_OK) err = r;
         }
     }
-    if (NS == 1 && !BIG && in_lds && FSEHIP_DEC1_TX) {
+    if (NS == 1 && !BIG && in_lds) {
         // 1-state: the same transposed stores, 64 symbols (one 64-byte piece)
         // per group, two chain steps per packed pair
         constexpr uint32_t G1 = 2u * DEC_GROUP;
@@ -1121,208 +905,6 @@ __global__ __launch_bounds__(64) void dtable_blocks_kernel(DtParams P) {
     if (lane == 0) P.dtinfo[gb] = rc == FSE_OK ? (int32_t)((uint32_t)hl | (L << 16)) : rc;
 }
 
-// ------------------------------------------------------------------------
-// The same decode tables from hdr_parse_kernel's counts, one 256-thread
-// workgroup per block at L <= 11 (fse.rs:280-338 with the spread of
-// fse.rs:110-162): the table kernel above runs every step on one wave
-// (~45K cycles per table at full occupancy, latency-bound); here each step
-// is spread over 4 waves, one symbol or 8 positions per thread, with the
-// wave scans joined through LDS:
-//   1. per symbol (thread = symbol): the -1 / positive counts, block-wide
-//      exclusive sums -> start marks of each symbol's occurrences, the -1
-//      symbols from the top of the table;
-//   2. forward max-fill of the marks: owner of occurrence j;
-//   3. the spread walk, 8 multipliers per thread: position (m * step) & mask
-//      is kept iff <= the high threshold, the j-th kept gets occurrence j;
-//   4. ranks: per 64-position chunk, each symbol's count (ballot peer
-//      matching) -> per-symbol prefix over the chunks (thread = symbol),
-//      with the symbol's first x (norm, or 1 for -1) folded in -> entry of
-//      position i from x = prefix + peers below, stored coalesced.
-// ------------------------------------------------------------------------
-// Measured slower than the one-wave kernel on C2 (0.132 vs 0.100 ms with
-// the header parse; profiles/r05/dtable_par/): 19.3K cycles per table at 7
-// workgroups per CU (its 16 KB rank table) against ~60K at 21 one-wave
-// workgroups per CU -- the ballot peer matching of pass 1 (6.4K) and the
-// dependent loads of step 1 (5.1K) keep the latency up.  Diagnostics build
-// only (FSEHIP_DT_PAR=1), kept as the recorded alternative.
-#if FSEHIP_DIAG
-template <int LMAX>
-__global__ __launch_bounds__(256) void dtable_par_kernel(DtParams P) {
-    static_assert(LMAX <= 11, "ranks of 2^LMAX / 64 chunks x 256 symbols in LDS");
-    constexpr uint32_t NT = 256, NW = NT / 64u, SIZE = 1u << LMAX, NCH = SIZE / 64u;
-    __shared__ __attribute__((aligned(16))) uint8_t sym_at[SIZE];
-    __shared__ __attribute__((aligned(16))) uint8_t occ[SIZE];
-    __shared__ __attribute__((aligned(16))) uint16_t rk[NCH * 256u];
-    __shared__ uint32_t xs[4 * NW];
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-    const uint64_t gb = blockIdx.x;
-    if (gb >= P.n_blocks) return;
-    FSE_STAMP(P, 0);
-    const uint8_t* in = P.in + gb * P.slot_bytes;
-    const uint32_t clen = P.comp_len[gb];
-    const uint32_t last = (clen && clen <= P.slot_bytes) ? in[clen - 1u] : 0u;
-    const int2 m = P.hdr_meta[gb];
-    const int hl = m.x;
-    const uint32_t L = (uint32_t)m.y & 0xFFu, tl = (uint32_t)m.y >> 8;
-    // the header's own status gates the build; the marker and length checks
-    // (lib.rs:222) wait for the marker byte's load, which lands meanwhile
-    int rc = hl < 0 ? hl : FSE_OK;
-    if (rc == FSE_OK && L > (uint32_t)LMAX) rc = FSE_ERR_UNSUPPORTED;
-    // (block-uniform from here on: every thread read the same words)
-    const uint32_t size = 1u << L, mask = size - 1u;
-    // 1. one symbol per thread
-    const uint32_t s = tid;
-    const uint32_t q = P.hdr_norm[gb * 128u + (s >> 1)];
-    const int32_t v = rc == FSE_OK && s < tl ? (int32_t)(int16_t)(q >> (16u * (s & 1u))) : 0;
-    const uint32_t neg = v < 0 ? 1u : 0u, pos = v > 0 ? (uint32_t)v : 0u;
-    const uint32_t ip = wave_incl_sum(pos), in_ = wave_incl_sum(neg);
-    if (lane == 63) {
-        xs[wv] = ip;
-        xs[NW + wv] = in_;
-    }
-    for (uint32_t i = tid; i < SIZE / 16u; i += NT) reinterpret_cast<uint4*>(occ)[i] = make_uint4(0, 0, 0, 0);
-    for (uint32_t i = tid; i < NCH * 256u / 8u; i += NT) reinterpret_cast<uint4*>(rk)[i] = make_uint4(0, 0, 0, 0);
-    __syncthreads();
-    uint32_t ep = ip - pos, en = in_ - neg, total_pos = 0, total_neg = 0;
-#pragma unroll
-    for (uint32_t w = 0; w < NW; ++w) {
-        ep += w < wv ? xs[w] : 0u;
-        en += w < wv ? xs[NW + w] : 0u;
-        total_pos += xs[w];
-        total_neg += xs[NW + w];
-    }
-    if (rc == FSE_OK && (total_pos + total_neg > size)) rc = FSE_ERR_BAD_TABLE;
-    const int32_t ht = (int32_t)size - 1 - (int32_t)total_neg;
-    if (rc == FSE_OK) {
-        if (pos) occ[ep] = (uint8_t)s;  // start mark of s's occurrences
-        if (neg) sym_at[size - 1u - en] = (uint8_t)s;  // -1 symbols from the top (fse.rs:122-125)
-    }
-    __syncthreads();
-    FSE_STAMP(P, 1);
-    // 2. forward max-fill over the occurrences, 8 per thread
-    {
-        uint2* o8 = reinterpret_cast<uint2*>(occ);
-        const bool in8 = tid * 8u < SIZE;
-        const uint2 w = in8 ? o8[tid] : make_uint2(0, 0);
-        uint32_t mx[8];
-#pragma unroll
-        for (uint32_t k = 0; k < 8; ++k) {
-            const uint32_t b = ((k < 4 ? w.x : w.y) >> (8u * (k & 3u))) & 0xFFu;
-            mx[k] = k ? max(mx[k - 1], b) : b;
-        }
-        const uint32_t incl = wave_incl_max(mx[7]);
-        if (lane == 63) xs[2 * NW + wv] = incl;
-        __syncthreads();
-        uint32_t carry = 0;
-#pragma unroll
-        for (uint32_t u = 0; u < NW; ++u) carry = u < wv ? max(carry, xs[2 * NW + u]) : carry;
-        const uint32_t b = max(carry, wave_shr1(incl));
-        uint32_t lo = 0, hi = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < 8; ++k) {
-            const uint32_t x = max(b, mx[k]) << (8u * (k & 3u));
-            if (k < 4) lo |= x; else hi |= x;
-        }
-        if (in8) o8[tid] = make_uint2(lo, hi);
-    }
-    __syncthreads();
-    FSE_STAMP(P, 2);
-    // 3. the spread walk, multipliers 8 * tid .. 8 * tid + 7 (fse.rs:139-150)
-    {
-        const uint32_t step = (size >> 3) * 5u + 3u;  // table_step (fse.rs:67-70)
-        uint32_t p[8], nv = 0;
-        bool keep[8];
-#pragma unroll
-        for (uint32_t k = 0; k < 8; ++k) {
-            const uint32_t mm = tid * 8u + k;
-            p[k] = (mm * step) & mask;
-            keep[k] = mm < size && (int32_t)p[k] <= ht;
-            nv += keep[k] ? 1u : 0u;
-        }
-        const uint32_t incl = wave_incl_sum(nv);
-        if (lane == 63) xs[3 * NW + wv] = incl;
-        __syncthreads();
-        uint32_t j = incl - nv, kept = 0;
-#pragma unroll
-        for (uint32_t u = 0; u < NW; ++u) {
-            j += u < wv ? xs[3 * NW + u] : 0u;
-            kept += xs[3 * NW + u];
-        }
-        if (rc == FSE_OK && kept != total_pos) rc = FSE_ERR_BAD_TABLE;  // position != 0 assert
-        if (rc == FSE_OK) {
-#pragma unroll
-            for (uint32_t k = 0; k < 8; ++k) {
-                if (keep[k] && j < total_pos) sym_at[p[k]] = occ[j];
-                j += keep[k] ? 1u : 0u;
-            }
-        }
-    }
-    __syncthreads();
-    FSE_STAMP(P, 3);
-    // after the header's status and before the table's, as the one-wave kernel orders them
-    if (hl >= 0 && L <= (uint32_t)LMAX) {
-        if ((uint32_t)hl >= clen || last == 0) rc = FSE_ERR_NO_MARKER;  // lib.rs:222
-        else if (clen > (1u << 28)) rc = FSE_ERR_UNSUPPORTED;  // bit positions are 32-bit in the decoders
-    }
-    if (rc != FSE_OK) {
-        if (tid == 0) P.dtinfo[gb] = rc;
-        return;
-    }
-    // 4a. per chunk t (64 positions; wave wv takes t = wv, wv + NW, ...):
-    // each symbol's count, and each lane's peers below (the chunks' symbols
-    // are read first, all in flight at once)
-    const uint32_t nch = size >= 64u ? size / 64u : 1u, kb = key_bits(tl);
-    constexpr uint32_t CPW = (NCH + NW - 1u) / NW;  // chunks per wave
-    uint32_t below[CPW], sy[CPW];
-#pragma unroll
-    for (uint32_t c = 0; c < CPW; ++c) {
-        const uint32_t i = (wv + c * NW) * 64u + lane;
-        sy[c] = i < size ? sym_at[i] : 0u;
-    }
-#pragma unroll
-    for (uint32_t c = 0; c < CPW; ++c) {
-        const uint32_t t = wv + c * NW;
-        below[c] = 0;
-        if (t < nch) {
-            const bool act = t * 64u + lane < size;
-            const uint64_t peers = match_key(sy[c], __ballot(act), kb);
-            below[c] = (uint32_t)__popcll(peers & lanemask_lt());
-            if (act && below[c] == 0) rk[t * 256u + sy[c]] = (uint16_t)__popcll(peers);
-        }
-    }
-    __syncthreads();
-    FSE_STAMP(P, 4);
-    // 4b. per symbol (thread = symbol): prefix over the chunks, starting at
-    // the symbol's first x (fse.rs:300-306: norm, or 1 for a -1 symbol)
-    if (s < tl) {
-        uint32_t run = v < 0 ? 1u : (uint32_t)v;
-        uint16_t c[NCH];
-#pragma unroll
-        for (uint32_t t = 0; t < NCH; ++t) c[t] = t < nch ? rk[t * 256u + s] : 0;
-#pragma unroll
-        for (uint32_t t = 0; t < NCH; ++t) {
-            if (t < nch) rk[t * 256u + s] = (uint16_t)run;
-            run += c[t];
-        }
-    }
-    __syncthreads();
-    FSE_STAMP(P, 5);
-    // 4c. entries (fse.rs:329-337), one coalesced store per chunk
-    uint32_t* dt = P.dt + gb * (uint64_t)SIZE;
-#pragma unroll
-    for (uint32_t c = 0; c < CPW; ++c) {
-        const uint32_t t = wv + c * NW;
-        const uint32_t i = t * 64u + lane;
-        if (t < nch && i < size) {
-            const uint32_t nx = (uint32_t)rk[t * 256u + sy[c]] + below[c];
-            const uint32_t nb = L - ilog2u(nx);
-            dt[i] = Dte<LMAX>::make(nb, sy[c], (nx << nb) - size);
-        }
-    }
-    if (tid == 0) P.dtinfo[gb] = (int32_t)((uint32_t)hl | (L << 16));
-    FSE_STAMP(P, 8);
-}
-#endif  // FSEHIP_DIAG
 
 // ------------------------------------------------------------------------
 // fse_decompress (lib.rs:187-211) without a sidecar: one lane per block
@@ -2461,10 +2043,7 @@ hipError_t launch_single(const DecParams& P, uint32_t lmax, hipStream_t stream) 
 // ------------------------------------------------------------------------
 hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) {
     const dim3 g(P.n_blocks);
-    // in-workgroup tables: 2-state segment decode at L <= 11 only (FSEHIP_DEC_INWG builds)
-    const bool inwg = P.hdr_meta && P.hdr_norm;
-    if (inwg && !FSEHIP_DEC_INWG) return hipErrorInvalidValue;
-    if (inwg ? (!P.sidecar || P.nstates == 1 || lmax != 11) : (!P.dt || !P.dtinfo)) return hipErrorInvalidValue;
+    if (!P.dt || !P.dtinfo) return hipErrorInvalidValue;
     if (!P.sidecar) {  // serial: sidecar-less blocks, reference-mode host streams, sidecar recording
         if (P.nstates == 1) {
             if (lmax <= 11 && P.states && P.bulk && !P.sidecar_out) {  // symbols deferred, as below
@@ -2477,10 +2056,7 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
             else hipLaunchKernelGGL((decode1_serial_kernel<15>), g, dim3(64), 0, stream, P);
         } else if (lmax <= 11 && P.states && P.bulk && !P.sidecar_out) {
             // symbols deferred: 8 blocks per workgroup, 32 chains per CU, then the map
-            if (P.pass == 7u)  // diagnostics (FSEHIP_SERIAL_DW=2): two decode waves of 4 chains (measured slower)
-                hipLaunchKernelGGL((serial_ring_kernel<11, 8, 2, true, 2>), dim3((P.n_blocks + 7u) / 8u), dim3(192), 0, stream, P);
-            else  // the 8 chains in one wave
-                hipLaunchKernelGGL((serial_ring_kernel<11, 8, 2, true>), dim3((P.n_blocks + 7u) / 8u), dim3(128), 0, stream, P);
+            hipLaunchKernelGGL((serial_ring_kernel<11, 8, 2, true>), dim3((P.n_blocks + 7u) / 8u), dim3(128), 0, stream, P);
             hipLaunchKernelGGL((sym_map_kernel<11>), dim3(P.n_blocks), dim3(256), 0, stream, P);
         } else {
             // 6 (L <= 11) or 3 (L = 12) blocks per workgroup: 24 / 12 chains per CU (LDS-bound)
@@ -2539,12 +2115,6 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
             run(decode_pre_kernel<15, 16, 1, 0>, 0, 0);
         }
     } else {
-#ifdef FSEHIP_DEC_WINDOW  // A/B only: every block through the global-memory window reader (table-only LDS)
-        if (lmax <= 11 && wide) {
-            run(decode_pre_kernel<11, 16, 2, 0, 512>, 0, 0, 512);
-            return hipGetLastError();
-        }
-#endif
         if (lmax <= 11 && wide) {
             run(decode_pre_kernel<11, PP, 2, 1, 512>, 1, 0, 512);
             run(decode_pre_kernel<11, PB, 2, 2, 512>, 2, 2, 512);
@@ -2596,14 +2166,6 @@ int occupancy_report_dec(char* buf, int cap) {
     return len;
 }
 
-hipError_t launch_hdr_parse(const DtParams& P, uint32_t lmax, hipStream_t stream) {
-    if (lmax > 12 || !P.hdr_meta || !P.hdr_norm) return hipErrorInvalidValue;
-    const dim3 gp((P.n_blocks + HP_BLOCKS - 1u) / HP_BLOCKS);
-    if (lmax <= 11) hipLaunchKernelGGL((hdr_parse_kernel<11>), gp, dim3(64), 0, stream, P);
-    else hipLaunchKernelGGL((hdr_parse_kernel<12>), gp, dim3(64), 0, stream, P);
-    return hipGetLastError();
-}
-
 hipError_t launch_dtables(const DtParams& P0, uint32_t lmax, hipStream_t stream) {
     DtParams P = P0;
     P.peer_ranks = rank_order_ok() ? 0u : 1u;
@@ -2616,10 +2178,6 @@ hipError_t launch_dtables(const DtParams& P0, uint32_t lmax, hipStream_t stream)
         P.hdr_meta = nullptr;
     }
     const dim3 g(P.n_blocks), b(64);
-#if FSEHIP_DIAG
-    if (lmax <= 11 && P.hdr_meta && P.par) hipLaunchKernelGGL((dtable_par_kernel<11>), g, dim3(256), P.xlds, stream, P);
-    else
-#endif
     if (lmax <= 11) hipLaunchKernelGGL((dtable_blocks_kernel<11>), g, b, P.xlds, stream, P);
     else if (lmax <= 12) hipLaunchKernelGGL((dtable_blocks_kernel<12>), g, b, P.xlds, stream, P);
     else if (lmax <= 13) hipLaunchKernelGGL((dtable_blocks_kernel<13>), g, b, P.xlds, stream, P);

@@ -13,10 +13,19 @@
 
 namespace fsehip {
 
-// Diagnostic phase stamps (only when P.stamps is set by the host).
+// Diagnostics (the libfsehip_diag.so build, -DFSEHIP_DIAG=1, for tools/ only):
+// phase stamps when P.stamps is set by the host, and the encoder's phase
+// ablations (FSE_ABLATE, EncParams::debug).  Both compile to nothing in the
+// product library.
+#ifdef FSEHIP_DIAG
+constexpr bool kDiag = true;
+#else
+constexpr bool kDiag = false;
+#endif
+#define FSE_ABLATE(P, bits) (kDiag && ((P).debug & (bits)) != 0u)
 #define FSE_STAMP(P, slot)                                                                     \
     do {                                                                                       \
-        if ((P).stamps && threadIdx.x == 0)                                                    \
+        if (kDiag && (P).stamps && threadIdx.x == 0)                                           \
             (P).stamps[(uint64_t)blockIdx.x * kStamps + (slot)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 

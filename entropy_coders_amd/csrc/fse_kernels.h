@@ -59,12 +59,6 @@ struct DecParams {
     // map kernel turns the states into symbols.
     uint32_t* states;
     uint32_t* bulk;
-    // In-workgroup decode tables (segment decode, 2-state, table log <= 11):
-    // with dt == nullptr the decode workgroup builds its block's table in LDS
-    // from hdr_parse_kernel's output (hdr_meta / hdr_norm, DtParams layout)
-    // while its image is staged, instead of staging a prebuilt table.
-    const int2* hdr_meta;
-    const uint32_t* hdr_norm;
 };
 
 // Decode-table build (header parse + DecodeTable) for a batch of blocks.
@@ -83,9 +77,6 @@ struct DtParams {
     // status, L | table_len << 8}; hdr_norm[b] = 256 x int16 counts (128 words).
     int2* hdr_meta;
     uint32_t* hdr_norm;
-    // diagnostics build only (FSEHIP_DT_PAR=1): with hdr_meta at L <= 11, the
-    // 4-wave table kernel (dtable_par_kernel, a measured negative) instead
-    uint32_t par;
     uint32_t peer_ranks;  // set by launch_dtables: 1 = peer-mask ranks (rank_order_ok() failed)
 };
 constexpr uint64_t hdr_scratch_bytes(uint64_t n_blocks) { return n_blocks * (512u + 8u); }
@@ -124,9 +115,6 @@ hipError_t launch_table(const fse_norm_histogram* nh, int enc, fse_encode_table*
 // rank_order_ok() runs it once per device and caches the answer (false on
 // any error), and the launchers fall back to peer-mask ranks when false.
 hipError_t rank_order_check(uint32_t* violations, uint64_t* atomics);
-// hdr_parse_kernel alone (P.hdr_meta / P.hdr_norm set, lmax <= 12): the
-// header scratch for the in-workgroup table builds of the segment decode.
-hipError_t launch_hdr_parse(const DtParams& P, uint32_t lmax, hipStream_t stream);
 bool rank_order_ok();
 // Tests: -1 = checked (default), 0 = atomic ranks, 1 = peer-mask ranks; returns the previous mode.
 int rank_mode(int mode);

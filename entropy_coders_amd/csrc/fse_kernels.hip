@@ -39,24 +39,14 @@ __device__ __forceinline__ uint4 load_chunk(const uint8_t* blk, uint32_t n, uint
 // stateTable[deltaFindState]} (fse.rs:165-188): the block's table base is
 // folded into the transform, so one state step is add, shift, shift-add,
 // ds_read_u16 whichever table of the workgroup the lane uses.
-#ifndef FSEHIP_ENC_ABL
-#define FSEHIP_ENC_ABL 0  // encoder timing probes (variant builds only)
-#endif
-#ifndef FSEHIP_ENC_PF
-#define FSEHIP_ENC_PF 4  // source chunk registers of the emit pass (PF - 1 loads in flight)
-#endif
+constexpr int ENC_PF = 4;  // source chunk registers of a pass (PF - 1 loads in flight; 6 and 8 measured the same)
 struct EncTab {
     const uint2* tt;  // {deltaNbBits, LDS address of stateTable + 2 * deltaFindState}
 };
 typedef __attribute__((address_space(3))) const uint16_t lds_cu16;
 typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
 __device__ __forceinline__ uint32_t st_at(uint32_t lds_addr) {
-#if FSEHIP_ENC_ABL & 32  // A/B: the entry's dword read whole (ds_read_b32) and its half extracted
-    const uint32_t v = *(lds_cu32*)(uintptr_t)(lds_addr & ~3u);
-    return __builtin_amdgcn_ubfe(v, (lds_addr & 2u) << 3, 16u);
-#else
     return *(lds_cu16*)(uintptr_t)lds_addr;
-#endif
 }
 // LDS byte address of a __shared__ object
 template <class P>
@@ -82,10 +72,7 @@ __device__ __forceinline__ uint32_t lds_addr_of(P* p) {
 // holds the pending group's 16 words plus <= 8 more: 24 slots, word w at
 // slot w mod 24 (a group's four 4-word pieces are 4-aligned slots, since
 // 16 g mod 24 is a multiple of 8).
-#ifndef FSEHIP_ENC_RING
-#define FSEHIP_ENC_RING 24  // emit ring words per lane (A/B builds: 32)
-#endif
-constexpr uint32_t RING_WORDS = FSEHIP_ENC_RING;
+constexpr uint32_t RING_WORDS = 24;  // emit ring words per lane
 struct Emit {
     uint32_t lo, hi;    // pending bits: lo = the word being filled, hi = bits past it
     uint32_t nacc;
@@ -98,9 +85,6 @@ struct Emit {
     bool skip_head;
     uint32_t* gw;
     uint32_t* ring;     // LDS, RING_WORDS words, 16-byte aligned
-#if FSEHIP_ENC_ABL & 192
-    uint32_t probe = 0;  // LDS-split probes: their reads folded in here (never waited for per pair)
-#endif
     __device__ __forceinline__ void start(uint32_t* g, uint32_t off, uint32_t lim = 0xFFFFFFFFu,
                                           uint32_t* r = nullptr) {
         gw = g;
@@ -154,24 +138,13 @@ struct Emit {
             store_words(skip_head ? w0 + 1u : w0, base + 16u);
         } else if (base + 16u <= wlim) {
             const uint32_t r0 = base % RING_WORDS;
-#if FSEHIP_ENC_ABL & 1  // probe (timing only, wrong output): the same stores into the slot's first 2 KiB (L2-resident lines)
-            uint4* o = reinterpret_cast<uint4*>(gw + (base & 511u));
-#else
             uint4* o = reinterpret_cast<uint4*>(gw + base);
-#endif
 #pragma unroll
             for (uint32_t q = 0; q < 4; ++q) {
                 uint32_t rq = r0 + 4u * q;
                 rq = rq >= RING_WORDS ? rq - RING_WORDS : rq;
                 const uint4 a = *reinterpret_cast<const uint4*>(ring + rq);
-#if FSEHIP_ENC_ABL & 8  // probe (timing only, wrong output): the group's ring reads without its stores
-                asm volatile("; sink %0 %1 %2 %3" ::"v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w));
-                (void)o;
-#elif FSEHIP_ENC_ABL & 16  // A/B (timing only): non-temporal group stores
-                __builtin_nontemporal_store(u32x4{a.x, a.y, a.z, a.w}, reinterpret_cast<u32x4*>(o + q));
-#else
                 o[q] = a;
-#endif
             }
         }
     }
@@ -224,15 +197,11 @@ struct Ckpt {
     uint64_t q[CKQ];  // q[0] = the latest entry (lowest index)
 };
 
-enum { PASS_COUNT = 1, PASS_EMIT = 2, PASS_REPAIR = 3, PASS_ECOUNT = 4, PASS_EREPAIR = 5 };
-// PASS_ECOUNT / PASS_EREPAIR: the count and repair passes doing the emit
-// pass's bit packing and ring writes as well (timing probe FSEHIP_ENC_ABL & 2
-// only: the cost of an "emit from the guessed start, repair by re-emitting"
-// encoder, without its placement pass)
+enum { PASS_COUNT = 1, PASS_EMIT = 2, PASS_REPAIR = 3 };
 template <int MODE>
-constexpr bool emits() { return MODE == PASS_EMIT || MODE == PASS_ECOUNT || MODE == PASS_EREPAIR; }
+constexpr bool emits() { return MODE == PASS_EMIT; }
 template <int MODE>
-constexpr bool counts() { return MODE == PASS_COUNT || MODE == PASS_REPAIR || MODE == PASS_ECOUNT || MODE == PASS_EREPAIR; }
+constexpr bool counts() { return MODE == PASS_COUNT || MODE == PASS_REPAIR; }
 
 // Trajectory of a count pass, for convergence-based repair: the state pair
 // and running bit count after every ckc-th chunk (at most TRACK_SLOTS slots per lane,
@@ -244,8 +213,7 @@ constexpr bool counts() { return MODE == PASS_COUNT || MODE == PASS_REPAIR || MO
 // after the slot (cb: .x chain 0, .y chain 1): a pass writes its running
 // counts there, and track_fixup turns the slots it wrote into remaining
 // counts once the pass totals are known, so every slot stays consistent
-// with the lane's current trajectory.  Per-chain counts let a repair stop
-// each chain where it meets its record (enc_repair2).
+// with the lane's current trajectory.
 // Trajectory slots per lane.  16 (repairs stop sooner) measured slower
 // than 8 on C2: the count pass writes twice as many slots.
 constexpr uint32_t TRACK_SLOTS = 8;
@@ -275,22 +243,10 @@ struct EncState {
 // whose upper word is nb.  Callers take nb = sum >> 16, or (counting passes)
 // add the sums as packed 16-bit halves, so that nb's only use on the chain
 // is the shift and the compiler takes it as the sum's upper word there (SDWA
-// src0_sel:WORD_1): add, shift, shift-add, ds_read_u16.  FSEHIP_ENC_SDWA
-// forces that shift in every pass (A/B knob, measured no faster).
-#ifndef FSEHIP_ENC_SDWA
-#define FSEHIP_ENC_SDWA 0
-#endif
+// src0_sel:WORD_1): add, shift, shift-add, ds_read_u16.
 __device__ __forceinline__ uint32_t state_step(uint32_t& x, const uint2 t) {
     const uint32_t sum = t.x + x;
-#if FSEHIP_ENC_SDWA
-    uint32_t y;
-    asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD"
-        : "=v"(y)
-        : "v"(sum), "v"(x));
-    x = st_at((y << 1) + t.y);
-#else
     x = st_at(((x >> (sum >> 16)) << 1) + t.y);
-#endif
     return sum;
 }
 // Packed 16-bit add (v_pk_add_u16): the upper halves add without a carry in
@@ -373,9 +329,6 @@ __device__ __forceinline__ void enc_chunk(const uint4& q, uint32_t c8, uint32_t 
 // starts with its transforms landed instead of waiting for 16 LDS reads
 // (the state loop is latency-bound: that wait was one exposed LDS round
 // trip per 8 pairs).  Same registers, same instruction count.
-#ifndef FSEHIP_ENC_TTPF
-#define FSEHIP_ENC_TTPF 1
-#endif
 __device__ __forceinline__ void tt_load(const uint4& q, uint2 (&t0)[8], uint2 (&t1)[8], const EncTab& T) {
     const uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
@@ -419,18 +372,6 @@ __device__ __forceinline__ void enc_chunk_pl(const uint4& qn, uint2 (&t0)[8], ui
         const uint32_t v1 = x1, v0 = x0;
         const uint32_t s1 = state_step(x1, t1[j]);
         const uint32_t s0 = state_step(x0, t0[j]);
-#if FSEHIP_ENC_ABL & 64  // LDS-split probe: one more stateTable gather per pair (chain 0's, one bank over; sunk)
-        {
-            const uint32_t a = (((v0 >> (s0 >> 16)) << 1) + t0[j].y) ^ 4u;
-            em.probe ^= st_at(a);
-        }
-#endif
-#if FSEHIP_ENC_ABL & 128  // LDS-split probe: one more transform gather per pair (the neighbour symbol's; sunk)
-        {
-            const uint2 e = T.tt[((wn[j >> 1] >> (16u * (uint32_t)(j & 1))) & 0xFFu) ^ 1u];
-            em.probe ^= e.x ^ e.y;
-        }
-#endif
         reload(j);
         const uint32_t nb1 = s1 >> 16, nb0 = s0 >> 16;
         if (PKB) {
@@ -487,7 +428,7 @@ template <int MODE, int NS>
 __device__ __forceinline__ EncState enc_range(const uint8_t* __restrict__ blk, uint32_t n, uint32_t pa, uint32_t pb,
                                               EncState st, const EncTab& T, Emit& em, Ckpt& ck, Track& tr) {
     constexpr bool TRACK = counts<MODE>();
-    constexpr bool RP = MODE == PASS_REPAIR || MODE == PASS_EREPAIR;
+    constexpr bool RP = MODE == PASS_REPAIR;
     uint32_t x0 = st.x0, x1 = st.x1, b0 = st.b0, b1 = st.b1;
     if (pb <= pa) return st;
     const uint4* v = reinterpret_cast<const uint4*>(blk);
@@ -536,23 +477,16 @@ __device__ __forceinline__ EncState enc_range(const uint8_t* __restrict__ blk, u
     if (c_hi < c_lo || (RP && tr.done)) return EncState{x0, x1, b0, b1};
     auto ld = [&](int32_t c) { return v[c < c_lo ? c_lo : c]; };
     // source chunks in flight: PF - 1 ahead of the one being encoded
-    constexpr int PF = emits<MODE>() ? FSEHIP_ENC_PF : 4;
+    constexpr int PF = ENC_PF;
     uint4 q[PF];
 #pragma unroll
     for (int k = 0; k < PF; ++k) q[k] = ld(c_hi - k);
-#if FSEHIP_ENC_TTPF
     uint2 t0[8], t1[8];  // the transforms of the chunk being encoded (tt_load / enc_chunk_pl)
     tt_load(q[0], t0, t1, T);
-#endif
     // qn: the next chunk's words (already loaded: PF - 1 chunks ahead)
     auto body = [&](const uint4& q, const uint4& qn, int32_t c) {
-#if FSEHIP_ENC_TTPF
         (void)q;
         enc_chunk_pl<MODE, NS>(qn, t0, t1, x0, x1, T, b0, b1, em);
-#else
-        (void)qn;
-        enc_chunk<MODE, true, NS>(q, (uint32_t)c << CS, pb, x0, x1, T, b0, b1, em);
-#endif
         if (emits<MODE>()) em.drain();
         if (MODE == PASS_EMIT && ck.base && (((uint32_t)c << CS) & ck.mask) == 0u)
             ckpt_record<NS>(ck, (uint32_t)c << CS, em.pos(), x0, x1);
@@ -573,93 +507,6 @@ __device__ __forceinline__ EncState enc_range(const uint8_t* __restrict__ blk, u
         if (done) break;
     }
     return EncState{x0, x1, b0, b1};
-}
-
-// Per-chain repair (NS = 2) of a lane below the top lane (whole chunks: S is
-// a multiple of 8).  The two states are independent chains (lib.rs:167-176),
-// so each chain whose start changed (bad0 / bad1) re-encodes from x0 / x1
-// only until it meets its own recorded trajectory at a slot, and a chunk
-// runs both chains while some lane of the wave still needs each, otherwise
-// only the one still needed (half the LDS gathers).  (A packed-pair test ran
-// both chains to the later of the two meetings, and both again when only
-// one start had changed: tools/chain_repair_sim.py.)  On return, for a chain
-// that was bad: tot_c = its bits over the lane; jc = the slot where it met
-// its record (-1: never, x_c is then its new end state); its slots above jc
-// hold running counts for the caller's fixup.
-// Measured slower (profiles/r05/enc_chain/enc_pc.txt): C2 1.64 against
-// 1.56 ms, skewed L = 12 6.87 against 5.90.  The step is latency-bound: a
-// chunk of one chain leaves each step's stateTable read with no second
-// chain to overlap, so it takes about as long as a chunk of both, and the
-// gathers it saves were not what the time waited on.  Off by default.
-#ifndef FSEHIP_ENC_PC
-#define FSEHIP_ENC_PC 0  // 1: per-chain repair (A/B); 0: packed-pair repair
-#endif
-template <int C>
-__device__ __forceinline__ void enc_chunk1(const uint4& q, uint32_t& x, uint32_t& b, const EncTab& T) {
-    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-    uint2 t[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) t[j] = T.tt[(w[j >> 1] >> (16u * (uint32_t)(j & 1) + 8u * C)) & 0xFFu];
-    uint32_t bacc = 0;
-#pragma unroll
-    for (int j = 7; j >= 0; --j) bacc = pk_add16(bacc, state_step(x, t[j]));
-    b += bacc >> 16;
-}
-
-__device__ __forceinline__ void enc_repair2(const uint8_t* __restrict__ blk, uint32_t pa, uint32_t pb, uint32_t& x0,
-                                            uint32_t& x1, bool bad0, bool bad1, const EncTab& T, Track& tr,
-                                            uint32_t& tot0, uint32_t& tot1, int32_t& j0, int32_t& j1) {
-    const uint4* v = reinterpret_cast<const uint4*>(blk);
-    const int32_t c_hi = (int32_t)((pb - 1u) >> 3), c_lo = (int32_t)(pa >> 3);
-    uint32_t rem = (uint32_t)(c_hi - c_lo) % tr.ckc, slot = (uint32_t)(c_hi - c_lo) / tr.ckc;
-    bool d0 = !bad0, d1 = !bad1;
-    j0 = j1 = -1;
-    uint32_t b0 = 0, b1 = 0;
-    Emit em;  // not written by counting chunks
-    auto ld = [&](int32_t c) { return v[c < c_lo ? c_lo : c]; };
-    uint4 q[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) q[k] = ld(c_hi - k);
-    for (int32_t c = c_hi;; c -= 4) {
-        bool out = false;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const bool n0 = __ballot(!d0) != 0ull, n1 = __ballot(!d1) != 0ull;  // wave-uniform
-            if (n0 && n1) enc_chunk<PASS_COUNT, true, 2>(q[k], 0u, pb, x0, x1, T, b0, b1, em);
-            else if (n0) enc_chunk1<0>(q[k], x0, b0, T);
-            else enc_chunk1<1>(q[k], x1, b1, T);
-            if (rem == 0u) {
-                const uint32_t r = tr.cx[slot];
-                const uint2 rb = tr.cb[slot];
-                if (!d0 && (r & 0xFFFFu) == x0) {  // from here on chain 0 is the recorded one
-                    d0 = true;
-                    j0 = (int32_t)slot;
-                    tot0 = b0 + rb.x;
-                }
-                if (!d1 && (r >> 16) == x1) {
-                    d1 = true;
-                    j1 = (int32_t)slot;
-                    tot1 = b1 + rb.y;
-                }
-                if (!d0 || !d1) {  // the chains still off their record rewrite their halves
-                    tr.cx[slot] = (d0 ? r & 0xFFFFu : x0) | (d1 ? r & 0xFFFF0000u : x1 << 16);
-                    tr.cb[slot] = make_uint2(d0 ? rb.x : b0, d1 ? rb.y : b1);
-                }
-                slot -= 1u;
-                rem = tr.ckc - 1u;
-            } else {
-                rem -= 1u;
-            }
-            if ((d0 && d1) || c - k - 1 < c_lo) {
-                out = true;
-                break;
-            }
-            q[k] = ld(c - k - 4);
-        }
-        if (out) break;
-    }
-    if (!d0) tot0 = b0;  // never met its record: the whole lane recounted
-    if (!d1) tot1 = b1;
 }
 
 // Encoder::new_first_symbol, fse.rs:210-218
@@ -749,9 +596,6 @@ struct EncSmem {
             } mg;
         } p2;
     } ph;
-#if FSEHIP_ENC_ABL & 2
-    uint32_t ring2[64 * RING_STRIDE];  // the probe's count / repair emit ring
-#endif
     int32_t info_status[BPW];
     uint32_t info_L[BPW];
     uint32_t info_hl[BPW];
@@ -759,34 +603,12 @@ struct EncSmem {
     int scratch[4];
 };
 
-// Pooled-repair timing probe (variant builds only; DESIGN.md section 5,
-// encoder item 10): two blocks per 128-thread workgroup, one wave each, with
-// a workgroup barrier after the count passes and after the repair, where a
-// pooled repair (one wave repairing both blocks' lanes from a job queue)
-// would have them.  1: both waves repair their own block (the layout's
-// cost); 2: wave 1 skips its repair (wrong output) and waits at the barrier
-// while wave 0 repairs: the time a pool could reach with one repair wave
-// per two blocks doing one block's repair steps.
-#ifndef FSEHIP_ENC_POOLPROBE
-#define FSEHIP_ENC_POOLPROBE 0
-#endif
 template <int LMAX, int T, int NS>
-constexpr int enc_nw() { return (FSEHIP_ENC_POOLPROBE && LMAX <= 11 && T == 64 && NS == 2) ? 2 : 1; }
-
-template <int LMAX, int T, int NS>
-__global__ __launch_bounds__((64 * enc_nw<LMAX, T, NS>())) void encode_blocks_kernel(EncParams P) {
+__global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     constexpr int BPW = 64 / T;
-#if FSEHIP_ENC_POOLPROBE
-    __shared__ EncSmem<LMAX, T> smv[enc_nw<LMAX, T, NS>()];
-    const uint32_t wv = enc_nw<LMAX, T, NS>() == 2 ? threadIdx.x >> 6 : 0u;
-    auto& sm = smv[wv];
-#define ENC_WGID ((uint64_t)blockIdx.x * enc_nw<LMAX, T, NS>() + wv)
-#define ENC_SYNC() wave_sync()
-#else
     __shared__ EncSmem<LMAX, T> sm;
 #define ENC_WGID ((uint64_t)blockIdx.x)
 #define ENC_SYNC() __syncthreads()
-#endif
     const uint32_t lane = lane_id();
 
     FSE_STAMP(P, 0);
@@ -805,7 +627,7 @@ __global__ __launch_bounds__((64 * enc_nw<LMAX, T, NS>())) void encode_blocks_ke
         const uint32_t tl = wave_histogram<Sm::HS>(
             blk, n, BPW == 1 ? sm.hist : reinterpret_cast<uint32_t*>(sm.st[b]), counts);
         FSE_STAMP(P, 1);
-        if (P.debug & 8u) {  // ablation: histogram only
+        if (FSE_ABLATE(P, 8u)) {  // ablation: histogram only
             if (lane == 0) P.status[gb] = (int32_t)tl;
             continue;
         }
@@ -900,7 +722,7 @@ __global__ __launch_bounds__((64 * enc_nw<LMAX, T, NS>())) void encode_blocks_ke
     }
 
     FSE_STAMP(P, 4);
-    if (P.debug & 9u) return;  // ablation: statistics + tables only (1), histogram only (8)
+    if (FSE_ABLATE(P, 9u)) return;  // ablation: statistics + tables only (1), histogram only (8)
     // ---- phase 2: T lanes per block
     const int b = BPW == 1 ? 0 : (int)(lane / T);
     const uint32_t k = BPW == 1 ? lane : lane % T;
@@ -942,12 +764,7 @@ __global__ __launch_bounds__((64 * enc_nw<LMAX, T, NS>())) void encode_blocks_ke
         // odd-length extra step), every other lane from a guessed start state,
         // recording its trajectory.  Then verify against the neighbour's end
         // state and repair by convergence (Track) until the fixed point.
-#if FSEHIP_ENC_ABL & 2
-        constexpr int MC = PASS_ECOUNT, MR = PASS_EREPAIR;
-        em.start(nullptr, pa * 24u, 0u, &sm.ring2[lane * RING_STRIDE]);
-#else
         constexpr int MC = PASS_COUNT, MR = PASS_REPAIR;
-#endif
         if (act) {
             EncState e0 = (k == ktop) ? top_start<PASS_COUNT, NS>(blk, n, tab, em)
                                       : EncState{start & 0xFFFFu, start >> 16, 0u, 0u};
@@ -959,15 +776,8 @@ __global__ __launch_bounds__((64 * enc_nw<LMAX, T, NS>())) void encode_blocks_ke
             track_fixup(tr, nslot, -1, tot0, tot1);
         }
         FSE_STAMP(P, 5);
-#if FSEHIP_ENC_POOLPROBE
-        __syncthreads();  // a pool starts once both blocks' count passes are done
-#endif
-        constexpr bool PC = NS == 2 && FSEHIP_ENC_PC && !(FSEHIP_ENC_ABL & 2);
         for (;;) {
-            if (P.debug & 16u) break;  // ablation: no repair (wrong output)
-#if FSEHIP_ENC_POOLPROBE == 2
-            if (wv == 1u) break;
-#endif
+            if (FSE_ABLATE(P, 16u)) break;  // ablation: no repair (wrong output)
             ENC_SYNC();
             bool bad0 = false, bad1 = false;
             uint32_t nbF = 0;
@@ -983,47 +793,24 @@ __global__ __launch_bounds__((64 * enc_nw<LMAX, T, NS>())) void encode_blocks_ke
             n_rerun += (uint32_t)__popcll(__ballot(bad));
             if (bad) {
                 start = nbF;
-                if constexpr (PC) {
-                    uint32_t x0 = start & 0xFFFFu, x1 = start >> 16;
-                    int32_t j0, j1;
-                    enc_repair2(blk, pa, pb, x0, x1, bad0, bad1, tab, tr, tot0, tot1, j0, j1);
-                    const bool nc0 = bad0 && j0 < 0, nc1 = bad1 && j1 < 0;  // met no record: a new end state
-                    if (nc0 || nc1) {
-                        myF = (nc0 ? x0 : myF & 0xFFFFu) | (nc1 ? x1 << 16 : myF & 0xFFFF0000u);
-                        sm.ph.p2.u.cntF[b][k] = myF;
-                    }
-                    for (int32_t j = (int32_t)nslot - 1; j >= 0; --j) {  // running -> remaining counts
-                        uint2 r = tr.cb[j];
-                        if (bad0 && j > j0) r.x = tot0 - r.x;
-                        if (bad1 && j > j1) r.y = tot1 - r.y;
-                        tr.cb[j] = r;
-                    }
-                } else {
-                    tr.done = false;
-#if FSEHIP_ENC_ABL & 2
-                    em.start(nullptr, pa * 24u, 0u, &sm.ring2[lane * RING_STRIDE]);
-#endif
-                    const EncState e0 = enc_range<MR, NS>(blk, n, pa, pb,
-                                                          EncState{start & 0xFFFFu, start >> 16, 0u, 0u}, tab, em, ck, tr);
-                    tot0 = e0.b0;
-                    tot1 = e0.b1;
-                    if (!tr.done) {  // did not converge: new end state
-                        myF = e0.x0 | (e0.x1 << 16);
-                        sm.ph.p2.u.cntF[b][k] = myF;
-                    }
-                    track_fixup(tr, nslot, tr.done ? (int32_t)tr.jstar : -1, tot0, tot1);
+                tr.done = false;
+                const EncState e0 = enc_range<MR, NS>(blk, n, pa, pb,
+                                                      EncState{start & 0xFFFFu, start >> 16, 0u, 0u}, tab, em, ck, tr);
+                tot0 = e0.b0;
+                tot1 = e0.b1;
+                if (!tr.done) {  // did not converge: new end state
+                    myF = e0.x0 | (e0.x1 << 16);
+                    sm.ph.p2.u.cntF[b][k] = myF;
                 }
+                track_fixup(tr, nslot, tr.done ? (int32_t)tr.jstar : -1, tot0, tot1);
             }
         }
-#if FSEHIP_ENC_POOLPROBE
-        __syncthreads();  // ... and ends once both blocks are repaired
-#endif
         bits = tot0 + tot1;
         if (k == 0) bits += (uint32_t)NS * L + 1u;  // finals + marker (lib.rs:178-181 / 139-141)
     }
 
     FSE_STAMP(P, 6);
-    if (P.stamps && lane == 0)
+    if (kDiag && P.stamps && lane == 0)
         P.stamps[(uint64_t)blockIdx.x * kStamps + kStamps - 1] = (uint64_t)n_iter | ((uint64_t)n_rerun << 32);
     // offsets: lane k writes after every lane j > k (stack order)
     const uint32_t hl = sm.info_hl[b];
@@ -1037,14 +824,14 @@ __global__ __launch_bounds__((64 * enc_nw<LMAX, T, NS>())) void encode_blocks_ke
     }
     const uint32_t total_bits = hdr_bits + __shfl(suffix, 0, T);
     const uint32_t off = hdr_bits + suffix - mybits;
-    const bool fits = (uint64_t)total_bits <= P.slot_bytes * 8ull && !(P.debug & 2u) && !(FSEHIP_ENC_ABL & 2);
+    const bool fits = (uint64_t)total_bits <= P.slot_bytes * 8ull && !FSE_ABLATE(P, 2u);
     uint32_t* gw = reinterpret_cast<uint32_t*>(P.out + gb * P.slot_bytes);
 
     // emit pass (its ring overlays the trajectories and end states: every
     // lane is past the repair rounds here)
     ENC_SYNC();
     if (act && fits) {
-        em.start(gw, off, (P.debug & 4u) ? 0u : (uint32_t)(P.slot_bytes >> 2),  // debug bit 2: no payload stores (ablation)
+        em.start(gw, off, FSE_ABLATE(P, 4u) ? 0u : (uint32_t)(P.slot_bytes >> 2),  // debug bit 2: no payload stores (ablation)
                  &sm.ph.p2.ring[lane * RING_STRIDE]);
         {
             if (P.sidecar && P.ckpt_interval) {
@@ -1134,9 +921,6 @@ __global__ __launch_bounds__((64 * enc_nw<LMAX, T, NS>())) void encode_blocks_ke
         if (fits) {
             P.status[gb] = FSE_OK;
             P.comp_len[gb] = (total_bits + 7u) >> 3;
-#if FSEHIP_ENC_ABL & 192
-            if (em.probe == 0x9E37u + (uint32_t)P.n_blocks * 0x10000u) P.comp_len[gb] = 0;  // keeps the probe reads (never true)
-#endif
             if (P.payload_bits) P.payload_bits[gb] = total_bits - hdr_bits;
         } else {
             P.status[gb] = FSE_ERR_DST_TOO_SMALL;
@@ -1289,9 +1073,7 @@ __global__ __launch_bounds__(256) void generate_kernel(GenParams G) {
 // ------------------------------------------------------------------------
 // launch wrappers
 // ------------------------------------------------------------------------
-#ifndef FSEHIP_ENC_WGS
-#define FSEHIP_ENC_WGS 11u  // resident encode workgroups per CU at L <= 11 (LDS-padded)
-#endif
+constexpr uint32_t ENC_WGS = 11u;  // resident encode workgroups per CU at L <= 11 (LDS-padded)
 hipError_t launch_encode(const EncParams& P0, uint32_t lmax, hipStream_t stream) {
     EncParams P = P0;
     P.peer_ranks = rank_order_ok() ? 0u : 1u;
@@ -1317,15 +1099,9 @@ hipError_t launch_encode(const EncParams& P0, uint32_t lmax, hipStream_t stream)
             hipFuncAttributes fa{};
             if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(encode_blocks_kernel<11, 64, 2>)) != hipSuccess)
                 return 0u;
-            const size_t per = (160u << 10) / FSEHIP_ENC_WGS - 64u;  // LDS per workgroup for 11, less allocation slack
+            const size_t per = (160u << 10) / ENC_WGS - 64u;  // LDS per workgroup for 11, less allocation slack
             return fa.sharedSizeBytes < per ? (uint32_t)(per - fa.sharedSizeBytes) : 0u;
         }();
-#if FSEHIP_ENC_POOLPROBE
-        if (lmax <= 11) {
-            hipLaunchKernelGGL((encode_blocks_kernel<11, 64, 2>), dim3((P.n_blocks + 1u) / 2u), dim3(128), 0, stream, P);
-            return hipGetLastError();
-        }
-#endif
         if (lmax <= 11) go(encode_blocks_kernel<11, 64, 2>, pad11);
         else if (lmax <= 12) go(encode_blocks_kernel<12, 64, 2>);
         else if (lmax <= 13) go(encode_blocks_kernel<13, 64, 2>);
