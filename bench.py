@@ -810,8 +810,14 @@ def main():
         ok = ok and h_ok
         del host_src, hs_stream, h_out, c_out, d_out
 
+    # every table of the run checked its atomic ranks (fse_device.hpp
+    # wave_build_spread); a fallback is a table rebuilt with peer-mask ranks
+    rank_check = codec.rank_fallbacks()
     if rank == 0:
         line = step_line()
+        line["rank_check"] = {"fallback_tables": rank_check,
+                              "what": "tables of this run (all of them check their LDS-atomic ranks) rebuilt with "
+                                      "peer-mask ranks because the check failed; 0 on a correct GPU"}
         if c3 is not None:
             line["c3_decode_only"] = c3
         if serial is not None:

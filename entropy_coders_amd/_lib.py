@@ -30,7 +30,7 @@ EXPORTS = (
     "fsehip_pack_blocks", "fsehip_unpack_blocks",
     "fsehip_dtable_bytes", "fsehip_build_dtables", "fsehip_decompress_blocks_dt",
     "fse_compress", "fse_decompress", "fsehip_sidecar_per_block_ns", "fse_decompress2_many", "fse_decompress_many",
-    "fsehip_copy_blocks", "fsehip_release_workspace",
+    "fsehip_copy_blocks", "fsehip_release_workspace", "fsehip_rank_fallbacks",
     "histogram_new", "histogram_normalize", "histogram_normalize_optimal", "norm_histogram_new",
     "norm_histogram_write", "norm_histogram_read", "encode_table_new", "decode_table_new", "fse_compress_nh",
     "bitstack_write", "bitstack_read", "bitstream_read", "bitstream_read_ops",
@@ -154,6 +154,7 @@ def load() -> C.CDLL:
     lib.fsehip_unpack_blocks.argtypes = [P, P, P, u32, P, u64, P]
     lib.fsehip_copy_blocks.argtypes = [P, P, P, u32, P, P, P]
     lib.fsehip_release_workspace.argtypes = [C.c_int, P]
+    lib.fsehip_rank_fallbacks.argtypes = [C.c_int, C.POINTER(u32 * 3), C.c_int]
     H, NH = C.POINTER(Histogram), C.POINTER(NormHistogram)
     lib.histogram_new.argtypes = [P, sz, H]
     lib.histogram_normalize.argtypes = [H, u32, NH]

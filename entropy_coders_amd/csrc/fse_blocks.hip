@@ -22,6 +22,18 @@
 
 namespace fsehip {
 
+// Tables of this file's kernels whose atomic ranks failed their check and
+// were rebuilt with the peer-mask ranks (wave_build_spread); per device.
+__device__ uint32_t g_rank_fb_tab;
+hipError_t rank_fallbacks_tab(uint32_t* out, bool reset) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rank_fb_tab), 4, 0, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && reset) {
+        const uint32_t z = 0;
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_rank_fb_tab), &z, 4, 0, hipMemcpyHostToDevice);
+    }
+    return e;
+}
+
 // ------------------------------------------------------------------------
 // Normalisation: mode 0 = Histogram::normalize(log2), 1 = normalize_optimal
 // (optimal_log2 first), 2 = NormHistogram::new from raw bytes.
@@ -153,7 +165,7 @@ __global__ __launch_bounds__(64) void table_kernel(const fse_norm_histogram* nh,
                 et->table[r] = (uint16_t)(size + i);  // fse.rs:157-162 (r = cumul[s] + rank)
                 et->symbols[i] = (uint8_t)s;
             },
-            [&](uint32_t s) { return (uint32_t)cumul[s]; }, peer_ranks == 0u);
+            [&](uint32_t s) { return (uint32_t)cumul[s]; }, RankAtomic{peer_ranks == 0u, occ, nullptr, 0u, &g_rank_fb_tab, 0u});
         // symbol transforms (fse.rs:165-188); total before symbol s = cumul[s]
         for (uint32_t s = lane; s < 256u; s += WAVE) {
             uint32_t bits = 0;
@@ -189,7 +201,7 @@ __global__ __launch_bounds__(64) void table_kernel(const fse_norm_histogram* nh,
             const int32_t v = norm[s];
             return v < 0 ? 1u : (uint32_t)v;
         },
-        peer_ranks == 0u);
+        RankAtomic{peer_ranks == 0u, occ, nullptr, 0u, &g_rank_fb_tab, 0u});
         uint32_t big = 0;  // fast_mode: no norm >= 2^(L-1) (fse.rs:302-305)
         for (uint32_t s = lane; s < tl; s += WAVE)
             if (norm[s] > 0 && (uint32_t)norm[s] >= (1u << (L - 1u))) big = 1;
@@ -423,7 +435,7 @@ hipError_t launch_hdr_read(const uint8_t* src, uint32_t n, fse_norm_histogram* o
 }
 hipError_t launch_table(const fse_norm_histogram* nh, int enc, fse_encode_table* et, fse_decode_table* dt, int32_t* status,
                         hipStream_t s) {
-    hipLaunchKernelGGL(table_kernel, dim3(1), dim3(64), 0, s, nh, enc, et, dt, status, rank_order_ok() ? 0u : 1u);
+    hipLaunchKernelGGL(table_kernel, dim3(1), dim3(64), 0, s, nh, enc, et, dt, status, atomic_ranks_on() ? 0u : 1u);
     return hipGetLastError();
 }
 
@@ -493,29 +505,10 @@ hipError_t rank_order_check(uint32_t* violations, uint64_t* atomics) {
     return hipSuccess;
 }
 
-static std::atomic<int> g_rank_mode{-1};  // fsehipx_rank_mode: -1 checked, 0 atomic, 1 peer-mask
+static std::atomic<int> g_rank_mode{-1};  // fsehipx_rank_mode: -1 / 0 atomic (checked per table), 1 peer-mask
 int rank_mode(int mode) { return g_rank_mode.exchange(mode); }
 
-bool rank_order_ok() {
-    const int forced = g_rank_mode.load(std::memory_order_relaxed);
-    if (forced >= 0) return forced == 0;
-    static std::atomic<int> state[64];  // per device: 0 unknown, 1 ok, 2 failed (or could not run)
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
-    int st = state[dev].load(std::memory_order_acquire);
-    if (st == 0) {
-        static std::mutex mu;
-        std::lock_guard<std::mutex> g(mu);
-        st = state[dev].load(std::memory_order_relaxed);
-        if (st == 0) {
-            uint32_t v = 1;
-            uint64_t n = 0;
-            st = (rank_order_check(&v, &n) == hipSuccess && v == 0 && n > 0) ? 1 : 2;
-            state[dev].store(st, std::memory_order_release);
-        }
-    }
-    return st == 1;
-}
+bool atomic_ranks_on() { return g_rank_mode.load(std::memory_order_relaxed) != 1; }
 
 hipError_t launch_host_return(const void* meta, const uint8_t* src, const uint32_t* len, void* hmeta, uint8_t* hdst,
                               uint32_t max, hipStream_t s) {

@@ -441,6 +441,7 @@ int fsehip_compress_blocks(const fsehip_params* p, const uint8_t* d_src, uint64_
     P.lanes = (ns == 2 && env_u32("FSEHIP_ENC_LANES", 64) == 32) ? 32 : 64;
     P.debug = env_u32("FSEHIP_DEBUG", 0);
     P.xlds = env_u32("FSEHIP_ENC_XLDS", 0);  // diagnostics: occupancy probe
+    P.rank_inject = env_u32("FSEHIP_RANK_INJECT", 0);  // diagnostics: fault injection into the atomic ranks
     const size_t groups = (n_blocks * P.lanes + 63) / 64;
     P.stamps = g_stamps_enc.get(groups);
     hipError_t e = fsehip::launch_encode(P, lmax, static_cast<hipStream_t>(stream));
@@ -541,6 +542,7 @@ static int build_dtables_impl(const fsehip_params* p, const uint8_t* d_in, uint6
     D.dt = d_dtables;
     D.dtinfo = d_dtinfo;
     D.xlds = env_u32("FSEHIP_DT_XLDS", 0);  // diagnostics: occupancy probe
+    D.rank_inject = env_u32("FSEHIP_RANK_INJECT", 0);  // diagnostics: fault injection into the atomic ranks
     D.stamps = g_stamps_dt.get(n_blocks);
     hipError_t e = fsehip::launch_dtables(D, kern_lmax(p->max_table_log), static_cast<hipStream_t>(stream));
     if (D.stamps) g_stamps_dt.report("dtables", n_blocks, static_cast<hipStream_t>(stream));
@@ -972,34 +974,51 @@ static int decompress_many(const uint8_t* const* srcs, const size_t* src_lens, s
     if (n_streams > (1u << 24) || dst_stride > 0x7FFFFFFFull) return FSE_ERR_UNSUPPORTED;
     if (!device_ok()) return FSE_ERR_NO_DEVICE;
     const uint64_t out_stride = round_up(dst_stride, 16);
-    std::vector<size_t> single, group;
-    auto run_group = [&]() -> int {
-        if (group.empty()) return FSE_OK;
-        if (group.size() <= 2) {  // not worth the batch kernels' fixed cost
-            single.insert(single.end(), group.begin(), group.end());
-            group.clear();
+    // Groups by the header's table log (histogram.rs:438: the first nibble +
+    // 5): <= 11, 12 and 13..15 take the kernels and decode-table stride of
+    // their class, so one stream with a large (or corrupt) log neither moves
+    // the others off the L <= 11 kernels nor multiplies their table scratch;
+    // a nibble above 15 can only fail, on the single path.  A group is capped
+    // by its staging bytes and by its decode-table + header scratch.
+    std::vector<size_t> single, group[3];
+    uint64_t gmax[3] = {0, 0, 0};  // each group's largest staged stream
+    constexpr uint32_t kClassLog[3] = {11, 12, 15};
+    auto run_group = [&](int c) -> int {
+        std::vector<size_t>& g = group[c];
+        gmax[c] = 0;
+        if (g.empty()) return FSE_OK;
+        if (g.size() <= 2) {  // not worth the batch kernels' fixed cost
+            single.insert(single.end(), g.begin(), g.end());
+            g.clear();
             return FSE_OK;
         }
-        const int rc = decompress_batch(srcs, src_lens, group, dst, dst_stride, dst_lens, statuses, nstates);
-        group.clear();
+        const int rc = decompress_batch(srcs, src_lens, g, dst, dst_stride, dst_lens, statuses, nstates);
+        g.clear();
         return rc;
     };
-    uint64_t gmax = 0;  // the group's largest staged stream
     for (size_t i = 0; i < n_streams; ++i) {
         const size_t n = src_lens[i];
         if (n == 0 || !srcs[i] || n > kManyStream || n_streams <= 2 || out_stride > kManyStage / 4) {
             single.push_back(i);  // statuses and long streams: the single call's own path
             continue;
         }
-        const uint64_t in_s = round_up(n + 32, 256), g = std::max(gmax, in_s);
-        if (!group.empty() && (group.size() + 1) * std::max(g, out_stride) > kManyStage) {
-            if (int rc = run_group()) return rc;
-            gmax = 0;
+        const uint32_t L = (uint32_t)(srcs[i][0] & 15u) + LOG_MIN_HOST;
+        if (L > 15u) {
+            single.push_back(i);
+            continue;
         }
-        group.push_back(i);
-        gmax = std::max(gmax, in_s);
+        const int c = L <= 11u ? 0 : L == 12u ? 1 : 2;
+        const uint64_t in_s = round_up(n + 32, 256), gm = std::max(gmax[c], in_s);
+        const uint64_t per_table = fsehip_dtable_bytes(kClassLog[c]) + fsehip::hdr_scratch_bytes(1) + 8u;
+        const uint64_t m1 = group[c].size() + 1;
+        if (!group[c].empty() && (m1 * std::max(gm, out_stride) > kManyStage || m1 * per_table > kManyStage)) {
+            if (int rc = run_group(c)) return rc;
+        }
+        group[c].push_back(i);
+        gmax[c] = std::max(gmax[c], in_s);
     }
-    if (int rc = run_group()) return rc;
+    for (int c = 0; c < 3; ++c)
+        if (int rc = run_group(c)) return rc;
     for (size_t i : single) {
         size_t len = 0;
         const int32_t st = src_lens[i] == 0 ? FSE_ERR_EMPTY  // BitStreamReader::new asserts (stream_reader.rs:17)
@@ -1356,9 +1375,21 @@ int fsehipx_rank_order_check(uint32_t* violations, uint64_t* atomics) {
     return fsehip::rank_order_check(violations, atomics) == hipSuccess ? FSE_OK : FSE_ERR_HIP;
 }
 
+int fsehip_rank_fallbacks(int device, uint32_t counts[3], int reset) {
+    if (!counts) return FSE_ERR_BAD_ARG;
+    int prev = 0;
+    if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess) return FSE_ERR_NO_DEVICE;
+    const bool r = reset != 0;
+    const bool ok = fsehip::rank_fallbacks_enc(&counts[0], r) == hipSuccess &&
+                    fsehip::rank_fallbacks_dec(&counts[1], r) == hipSuccess &&
+                    fsehip::rank_fallbacks_tab(&counts[2], r) == hipSuccess;
+    (void)hipSetDevice(prev);
+    return ok ? FSE_OK : FSE_ERR_HIP;
+}
+
 // Diagnostics only: force the table builds' rank method (tests of the
-// fallback): -1 = the checked default, 0 = atomic ranks, 1 = peer-mask
-// ranks.  Returns the previous mode.
+// fallback): -1 / 0 = atomic ranks checked per table (the default), 1 =
+// peer-mask ranks.  Returns the previous mode.
 int fsehipx_rank_mode(int mode) { return fsehip::rank_mode(mode < 0 ? -1 : mode > 0 ? 1 : 0); }
 
 }  // extern "C"

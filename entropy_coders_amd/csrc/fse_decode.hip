@@ -29,6 +29,18 @@
 
 namespace fsehip {
 
+// Tables of this file's kernels whose atomic ranks failed their check and
+// were rebuilt with the peer-mask ranks (wave_build_spread); per device.
+__device__ uint32_t g_rank_fb_dec;
+hipError_t rank_fallbacks_dec(uint32_t* out, bool reset) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rank_fb_dec), 4, 0, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && reset) {
+        const uint32_t z = 0;
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_rank_fb_dec), &z, 4, 0, hipMemcpyHostToDevice);
+    }
+    return e;
+}
+
 // cache policy of the segment decoder's LDS-DMA staging loads: nt (2), as the image and table
 // are read once (C3 0.96 -> 0.91-0.96 ms, C2 decode 0.558 -> 0.552-0.554 ms, same box)
 constexpr int STAGE_AUX = 2;
@@ -895,11 +907,11 @@ __global__ __launch_bounds__(64) void dtable_blocks_kernel(DtParams P) {
             return v < 0 ? 1u : (uint32_t)v;
         };
         // two-pass ranks need 2^L / 64 per-chunk registers: up to L = 12
-        const bool atomic_ranks = P.peer_ranks == 0u;
+        const RankAtomic ra{P.peer_ranks == 0u, occ, nullptr, 0u, &g_rank_fb_dec, P.rank_inject};
         if (LMAX <= 12)
-            rc = wave_build_spread<SIZE / 64u>(norm, L, tl, sym_at, occ, cumul, cnt, visit, first_x, atomic_ranks, rk, pm,
+            rc = wave_build_spread<SIZE / 64u>(norm, L, tl, sym_at, occ, cumul, cnt, visit, first_x, ra, rk, pm,
                                                &P);
-        else rc = wave_build_spread(norm, L, tl, sym_at, occ, cumul, cnt, visit, first_x, atomic_ranks);
+        else rc = wave_build_spread(norm, L, tl, sym_at, occ, cumul, cnt, visit, first_x, ra);
     }
     FSE_STAMP(P, 8);
     if (lane == 0) P.dtinfo[gb] = rc == FSE_OK ? (int32_t)((uint32_t)hl | (L << 16)) : rc;
@@ -2168,7 +2180,7 @@ int occupancy_report_dec(char* buf, int cap) {
 
 hipError_t launch_dtables(const DtParams& P0, uint32_t lmax, hipStream_t stream) {
     DtParams P = P0;
-    P.peer_ranks = rank_order_ok() ? 0u : 1u;
+    P.peer_ranks = atomic_ranks_on() ? 0u : 1u;
     if (lmax > 12) P.hdr_meta = nullptr;  // the staged rows hold headers up to L = 12
     if (P.hdr_meta && P.hdr_norm) {
         const dim3 gp((P.n_blocks + HP_BLOCKS - 1u) / HP_BLOCKS);

@@ -720,10 +720,20 @@ struct NoStamps {
     uint64_t* stamps = nullptr;
 };
 
+// Atomic ranks (below) and how a table built with them checks itself.
+struct RankAtomic {
+    bool on;              // atomic ranks allowed (else the peer-mask ranks)
+    uint8_t* inv8;        // inverse mode: 2^L bytes of dead scratch (lane | last-in-chunk << 6 per slot)
+    const uint16_t* st;   // stateTable mode (inv8 == nullptr): the visit's stateTable, entries st_off + position
+    uint32_t st_off;
+    uint32_t* fallbacks;  // global count of tables whose check failed (rebuilt with peer-mask ranks), or nullptr
+    uint32_t inject;      // diagnostics build only: chunk 0's ranks in descending lane order (fault injection)
+};
+
 template <uint32_t MAXCH = 64, typename Visit, typename Base, class SP = NoStamps>  // MAXCH: 2^LMAX / 64 chunks (two-pass ranks)
 __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_t tl, uint8_t* sym_at,
                                         uint8_t* occ_sym, uint16_t* cumul, uint32_t* cnt, Visit visit, Base base,
-                                        bool atomic_ranks, uint16_t* RK = nullptr, uint64_t* PM = nullptr,
+                                        const RankAtomic& ra, uint16_t* RK = nullptr, uint64_t* PM = nullptr,
                                         const SP* SPp = nullptr) {
     // SPp: diagnostics only, a params struct with `stamps` (phase stamps 3..7)
 #define SPREAD_STAMP(k)                                  \
@@ -827,30 +837,92 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
     }
     wave_sync();
     SPREAD_STAMP(5);
-    if (atomic_ranks) {
-    // Ranks by one LDS atomic per 64 positions: the old values that a
-    // ds_add_rtn_u32 hands to the lanes of one instruction hitting the same
-    // counter come in ascending lane order on gfx950 (tools/micro/
-    // lds_atomic_order.hip: 1.5e9 atomics, uniform and skewed keys, partial
-    // exec masks, none out of order), and the instructions run in position
-    // order, so the value is the count of s at earlier positions -- the
-    // rank -- on top of the caller's base.  The property is not documented:
-    // the library checks it once per device (rank_order_check_kernel,
-    // fsehip_rank_order_check) and passes atomic_ranks = false, the peer-mask
-    // ranks below, if it ever fails.
-    for (uint32_t s = lane; s < 256u; s += WAVE) cnt[s] = base(s);
-    wave_sync();
-    for (uint32_t i0 = 0; i0 < size; i0 += WAVE) {
-        const uint32_t i = i0 + lane;
-        if (i < size) {
-            const uint32_t sy = sym_at[i];
-            const uint32_t r = __hip_atomic_fetch_add((lds_u32*)cnt + sy, 1u, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_WORKGROUP);
-            visit(i, sy, r);
+    if (ra.on) {
+        // Ranks by one LDS atomic per 64 positions: the old values that a
+        // ds_add_rtn_u32 hands to the lanes of one instruction hitting the
+        // same counter come in ascending lane order on gfx950 (tools/micro/
+        // lds_atomic_order.hip: 1.5e9 atomics, uniform and skewed keys,
+        // partial exec masks, none out of order), and a wave's LDS
+        // instructions run in order, so the value is the count of s at
+        // earlier positions -- the rank -- on top of the caller's base.  The
+        // lane order is not documented, so every table checks the result
+        // (below) and is rebuilt with the peer-mask ranks if it fails.
+        //
+        // Inverse mode (inv8): the counters carry the symbol's slot in the
+        // high half (cumul[s] + rank, the stateTable order of fse.rs:157-162)
+        // and base + rank in the low half, so one atomic gives both; slot g
+        // records the lane that took it and whether it was the last slot its
+        // chunk took for that symbol (the counter read back after the
+        // instruction).
+        const bool inv = ra.inv8 != nullptr;
+        const uint32_t step = inv ? 0x10001u : 1u;
+        for (uint32_t s = lane; s < 256u; s += WAVE) cnt[s] = inv ? ((uint32_t)cumul[s] << 16) | base(s) : base(s);
+        wave_sync();
+        for (uint32_t i0 = 0; i0 < size; i0 += WAVE) {
+            const uint32_t i = i0 + lane;
+            const bool act = i < size;
+            const uint32_t sy = act ? sym_at[i] : 0u;
+            uint32_t r = 0;
+            if (act)
+                r = __hip_atomic_fetch_add((lds_u32*)cnt + sy, step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (kDiag && ra.inject && i0 == 0) {  // fault injection: the lanes' order reversed
+                const uint64_t peers = match_key(sy, __ballot(act), key_bits(tl));
+                const uint32_t bl = (uint32_t)__popcll(peers & lanemask_lt()), k = (uint32_t)__popcll(peers);
+                r += (k - 1u - 2u * bl) * step;
+            }
+            if (act) {
+                if (inv) {
+                    const uint32_t g = r >> 16;
+                    const uint32_t end =
+                        __hip_atomic_load((lds_u32*)cnt + sy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >> 16;
+                    ra.inv8[g] = (uint8_t)(lane | (g + 1u == end ? 0x40u : 0u));
+                    visit(i, sy, r & 0xFFFFu);
+                } else {
+                    visit(i, sy, r);
+                }
+            }
         }
-    }
-    wave_sync();
-    return FSE_OK;
+        wave_sync();
+        // The check: the ranks of one symbol must follow its positions.  A
+        // wave's instructions keep their order, so only lanes of one
+        // instruction can be out of order, and only among themselves.
+        bool bad = false;
+        if (inv) {
+            // consecutive slots g, g + 1 of one chunk's range for one symbol
+            // (g not flagged last) must hold ascending lanes
+            for (uint32_t q0 = 0; q0 < size; q0 += 8u * WAVE) {
+                const uint32_t g = q0 + 8u * lane;
+                if (g < size) {
+                    const uint2 w = *reinterpret_cast<const uint2*>(ra.inv8 + g);
+                    const uint64_t b8 = ((uint64_t)w.y << 32) | w.x;
+                    const uint32_t nx = g + 8u < size ? (uint32_t)ra.inv8[g + 8u] : 0x40u;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const uint32_t cur = (uint32_t)(b8 >> (8 * j)) & 0xFFu;
+                        const uint32_t nxt = j < 7 ? (uint32_t)(b8 >> (8 * j + 8)) & 0xFFu : nx;
+                        bad |= !(cur & 0x40u) && (cur & 63u) >= (nxt & 63u);
+                    }
+                }
+            }
+        } else {
+            // the stateTable (slot -> st_off + position): positions ascend
+            // within a symbol's slots; a descent must be a symbol boundary
+            for (uint32_t q0 = 0; q0 < size; q0 += 4u * WAVE) {
+                const uint32_t g = q0 + 4u * lane;
+                if (g < size) {
+                    const uint2 w = *reinterpret_cast<const uint2*>(ra.st + g);
+                    const uint32_t v[5] = {w.x & 0xFFFFu, w.x >> 16, w.y & 0xFFFFu, w.y >> 16,
+                                           g + 4u < size ? (uint32_t)ra.st[g + 4u] : 0xFFFFFu};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (v[j] > v[j + 1] && sym_at[v[j] - ra.st_off] == sym_at[v[j + 1] - ra.st_off]) bad = true;
+                }
+            }
+        }
+        if (__ballot(bad) == 0ull) return FSE_OK;
+        if (lane == 0 && ra.fallbacks) atomicAdd(ra.fallbacks, 1u);
+        wave_sync();
+        // rebuilt below with the peer-mask ranks (every position visited again)
     }
     if (RK != nullptr && tl <= 64u && size >= WAVE) {
         // pass 1: per 64-position chunk t, each symbol's count at RK[t][s]

@@ -28,7 +28,8 @@ struct EncParams {
                      // bit3 = histogram only, bit4 = no repair rounds
     uint64_t* stamps;  // diagnostics: per-workgroup s_memtime at phase ends
     uint32_t xlds;            // diagnostics: extra dynamic LDS bytes per workgroup (occupancy probe)
-    uint32_t peer_ranks;      // set by launch_encode: 1 = peer-mask ranks (rank_order_ok() failed)
+    uint32_t peer_ranks;      // set by launch_encode: 1 = peer-mask ranks (forced by rank_mode)
+    uint32_t rank_inject;     // diagnostics build only: fault injection into the atomic ranks (FSEHIP_RANK_INJECT)
 };
 
 struct DecParams {
@@ -77,7 +78,8 @@ struct DtParams {
     // status, L | table_len << 8}; hdr_norm[b] = 256 x int16 counts (128 words).
     int2* hdr_meta;
     uint32_t* hdr_norm;
-    uint32_t peer_ranks;  // set by launch_dtables: 1 = peer-mask ranks (rank_order_ok() failed)
+    uint32_t peer_ranks;  // set by launch_dtables: 1 = peer-mask ranks (forced by rank_mode)
+    uint32_t rank_inject; // diagnostics build only: fault injection into the atomic ranks (FSEHIP_RANK_INJECT)
 };
 constexpr uint64_t hdr_scratch_bytes(uint64_t n_blocks) { return n_blocks * (512u + 8u); }
 
@@ -110,13 +112,19 @@ hipError_t launch_table(const fse_norm_histogram* nh, int enc, fse_encode_table*
                         int32_t* status, hipStream_t s);
 // The table builds rank positions with one LDS atomic per 64 positions,
 // which needs same-address ds_add_rtn_u32 results in ascending lane order
-// (fse_device.hpp wave_build_spread).  rank_order_check runs the check
-// kernel (synchronous; counts the violations among `atomics` checked);
-// rank_order_ok() runs it once per device and caches the answer (false on
-// any error), and the launchers fall back to peer-mask ranks when false.
+// (fse_device.hpp wave_build_spread).  Every table checks its own ranks and
+// is rebuilt with the peer-mask ranks when the check fails; the per-device
+// counts of such rebuilds: rank_fallbacks_enc (encode_blocks_kernel),
+// _dec (dtable_blocks_kernel), _tab (table_kernel), read and optionally reset.
+// rank_order_check runs a stand-alone probe of the lane order (synchronous;
+// counts the violations among `atomics` checked), for tests and tools only.
 hipError_t rank_order_check(uint32_t* violations, uint64_t* atomics);
-bool rank_order_ok();
-// Tests: -1 = checked (default), 0 = atomic ranks, 1 = peer-mask ranks; returns the previous mode.
+hipError_t rank_fallbacks_enc(uint32_t* out, bool reset);
+hipError_t rank_fallbacks_dec(uint32_t* out, bool reset);
+hipError_t rank_fallbacks_tab(uint32_t* out, bool reset);
+// false only when rank_mode forces the peer-mask ranks
+bool atomic_ranks_on();
+// Tests: -1 = default (atomic ranks, checked per table), 0 = the same, 1 = peer-mask ranks; returns the previous mode.
 int rank_mode(int mode);
 // Host-call return: the 16-byte record at meta and min(*len, max) bytes of
 // src into pinned host memory (hmeta, hdst; 16-byte aligned).

@@ -22,6 +22,18 @@
 
 namespace fsehip {
 
+// Tables of this file's kernels whose atomic ranks failed their check and
+// were rebuilt with the peer-mask ranks (wave_build_spread); per device.
+__device__ uint32_t g_rank_fb_enc;
+hipError_t rank_fallbacks_enc(uint32_t* out, bool reset) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rank_fb_enc), 4, 0, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && reset) {
+        const uint32_t z = 0;
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_rank_fb_enc), &z, 4, 0, hipMemcpyHostToDevice);
+    }
+    return e;
+}
+
 // ------------------------------------------------------------------------
 // small helpers
 // ------------------------------------------------------------------------
@@ -664,7 +676,8 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
                                    [&](uint32_t i, uint32_t, uint32_t r) {
                                        st[r] = (uint16_t)(size + i);  // fse.rs:157-162 (r = cumul[s] + rank)
                                    },
-                                   [&](uint32_t s) { return (uint32_t)cumul[s]; }, P.peer_ranks == 0u, nullptr,
+                                   [&](uint32_t s) { return (uint32_t)cumul[s]; },
+                                   RankAtomic{P.peer_ranks == 0u, nullptr, st, size, &g_rank_fb_enc, P.rank_inject}, nullptr,
                                    reinterpret_cast<uint64_t*>(&sm.tt[b][0]));
             // symbol transforms, fse.rs:165-188 (total == cumul[s]), with
             // the stateTable's LDS address folded into deltaFindState
@@ -1076,7 +1089,7 @@ __global__ __launch_bounds__(256) void generate_kernel(GenParams G) {
 constexpr uint32_t ENC_WGS = 11u;  // resident encode workgroups per CU at L <= 11 (LDS-padded)
 hipError_t launch_encode(const EncParams& P0, uint32_t lmax, hipStream_t stream) {
     EncParams P = P0;
-    P.peer_ranks = rank_order_ok() ? 0u : 1u;
+    P.peer_ranks = atomic_ranks_on() ? 0u : 1u;
     // 32 lanes per block (two blocks per wave) for L <= 12 when asked for;
     // L 13..15 tables (64 KiB stateTable) run one block per workgroup
     const uint32_t T = (P.lanes == 32 && lmax <= 12) ? 32u : 64u;

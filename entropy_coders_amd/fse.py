@@ -107,6 +107,8 @@ def decompress2_many(streams, dst_stride: int, nstates: int = 2, raw: bool = Fal
     passed in, n * dst_stride bytes, to reuse one buffer across calls)."""
     from ._lib import STATUS
 
+    if nstates not in (1, 2):
+        raise ValueError(f"nstates must be 1 or 2, not {nstates!r}")
     lib = load()
     bufs = [_buf(x) for x in streams]
     n = len(bufs)
@@ -114,6 +116,10 @@ def decompress2_many(streams, dst_stride: int, nstates: int = 2, raw: bool = Fal
     lens = np.array([len(b) for b in bufs] or [0], dtype=np.uintp)
     if dst is None:
         dst = np.empty(max(n, 1) * dst_stride, dtype=np.uint8)
+    elif not (isinstance(dst, np.ndarray) and dst.dtype == np.uint8 and dst.flags.c_contiguous
+              and dst.flags.writeable and dst.nbytes >= n * dst_stride):
+        # the C call writes n * dst_stride bytes through the raw pointer
+        raise ValueError(f"dst must be a writeable C-contiguous uint8 ndarray of >= {n * dst_stride} bytes")
     out_lens = np.zeros(max(n, 1), dtype=np.uintp)
     st = np.zeros(max(n, 1), dtype=np.int32)
     fn = lib.fse_decompress2_many if nstates == 2 else lib.fse_decompress_many
@@ -455,6 +461,17 @@ class BlockCodec:
         check(self.lib.fsehip_release_workspace(self.device.index if self.device.index is not None else
                                                 self.torch.cuda.current_device(), self._stream()),
               "fsehip_release_workspace")
+
+    def rank_fallbacks(self, reset: bool = False) -> dict:
+        """`fsehip_rank_fallbacks` on this codec's device: tables whose atomic
+        ranks failed their self-check and were rebuilt with peer-mask ranks
+        (batch encoder, decode-table builds, building-block table calls)."""
+        import ctypes as C
+
+        out = (C.c_uint32 * 3)()
+        dev = self.device.index if self.device.index is not None else self.torch.cuda.current_device()
+        check(self.lib.fsehip_rank_fallbacks(dev, C.byref(out), 1 if reset else 0), "fsehip_rank_fallbacks")
+        return {"encode": int(out[0]), "decode_tables": int(out[1]), "table_calls": int(out[2])}
 
     def n_blocks(self, n_total: int) -> int:
         return (n_total + self.block_size - 1) // self.block_size

@@ -472,6 +472,16 @@ int fsehip_histogram_blocks(const uint8_t* d_src, uint64_t n_total, uint32_t blo
 int fsehip_generate(int kind, double prob, uint64_t seed, uint32_t block_size, uint8_t* d_out,
                     uint64_t n_total, fsehip_stream_t stream);
 
+/* Self-check of the table builds.  Every stateTable and decode table ranks its
+ * positions with one LDS atomic per 64 positions (fse.rs:157-162, 329-337
+ * order), which relies on an undocumented lane order of same-address LDS
+ * atomics, so every table checks its ranks and is rebuilt with lane-matching
+ * ranks when the check fails.  counts[0..2] = the rebuilds so far on `device`
+ * by the batch encoder, the decode-table builds and the building-block table
+ * calls (0 on a correct GPU); reset != 0 zeroes them after reading.
+ * Synchronous. */
+int fsehip_rank_fallbacks(int device, uint32_t counts[3], int reset);
+
 /* Device count visible to this process (0 when HIP is unusable). */
 int fsehip_device_count(void);
 /* Library build identifier. */

@@ -113,3 +113,51 @@ def test_many_streams_mixed_sizes_and_groups(torch_cuda):
     # 96 MiB strides: 5 streams per 512 MiB staging group -> two groups
     got = decompress2_many([O.compress2(s)[0] for s in smalls] * 2, 96 << 20)
     assert got == [s.tobytes() for s in smalls] * 2
+
+
+def test_many_streams_log_classes(torch_cuda):
+    """Streams are grouped by the table log in their header (<= 11, 12,
+    13..15), so one L = 15 stream and one header whose log nibble is corrupt
+    (L > 15) do not move the other streams off the L <= 11 kernels or fail
+    the call: every stream gets its single-call result."""
+    from entropy_coders_amd import decompress2_many
+
+    smalls = [O.generate(0, 0.155, 0x5EED0002, i, 4096) for i in range(300)]
+    comps = [O.compress2(s)[0] for s in smalls]
+    l12 = O.generate(0, 0.155, 0x5EED0005, 0, 65536)
+    l15 = O.generate(2, 0.0, 0x5EED0006, 0, 65536).copy()
+    l15[-2:] = 250  # rare seeds: the crate's new_first_symbol panics at L = 15 on frequent ones
+    c12, c15 = O.compress2(l12, 12)[0], O.compress2(l15, 15)[0]
+    assert (c12[0] & 15) + 5 == 12 and (c15[0] & 15) + 5 == 15
+    bad = bytearray(comps[7])
+    bad[0] = (bad[0] & 0xF0) | 0x0F  # log nibble 15: L = 20
+    streams = comps[:100] + [c15] + comps[100:200] + [bytes(bad)] + [c12] + comps[200:]
+    got = decompress2_many(streams, 65536)
+    for i, (x, g) in enumerate(zip(streams, got)):
+        try:
+            want = O.decompress2(x, 65536)
+        except O.OracleError as e:
+            assert g == e.code, (i, e.code, g)
+            continue
+        assert g == want, i
+    assert got[100] == l15.tobytes() and got[202] == l12.tobytes()
+
+
+def test_many_rejects_bad_dst_and_nstates(torch_cuda):
+    """The Python mirror refuses an output buffer the C call would overrun
+    (too small, wrong dtype, strided, read-only) and an unknown format."""
+    from entropy_coders_amd import decompress2_many
+
+    comps = [O.compress2(O.generate(0, 0.155, 0x5EED0002, i, 4096))[0] for i in range(4)]
+    for dst in (np.empty(4 * 4096 - 1, np.uint8), np.empty(8 * 4096, np.uint8)[::2], np.empty(4 * 4096, np.uint16),
+                [0] * (4 * 4096)):
+        with pytest.raises(ValueError):
+            decompress2_many(comps, 4096, raw=True, dst=dst)
+    ro = np.empty(4 * 4096, np.uint8)
+    ro.flags.writeable = False
+    with pytest.raises(ValueError):
+        decompress2_many(comps, 4096, raw=True, dst=ro)
+    with pytest.raises(ValueError):
+        decompress2_many(comps, 4096, nstates=3)
+    d, lens, st = decompress2_many(comps, 4096, raw=True, dst=np.empty(4 * 4096, np.uint8))
+    assert (st == 0).all() and (lens == 4096).all()
