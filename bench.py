@@ -619,6 +619,9 @@ def main():
                 "ckpt_interval": f"{args.ckpt} {'pairs' if args.nstates == 2 else 'symbols'}",
                 "parallelism": f"dp{world} (blocks sharded per GPU, no collective in the step)",
             },
+            "timed_region": ("K encode + decode steps per rank on HBM-resident blocks, barrier + synchronize on "
+                             "both sides, max over ranks; no collective inside (the N > 1 gather / scatter is "
+                             "timed on its own in c4_exchange)"),
             # dominant kernel of the step: encode (one launch per step)
             "roofline": roofline("fse_encode_blocks", enc_ms, enc_bytes, "encode launch, HIP events", prof_cfg),
             "roofline_decode": roofline("fse_decode_blocks", dec_ms, dec_bytes,

@@ -25,12 +25,13 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, scheme, q, backend="gloo", NB=NB):
+def _worker(rank, world, port, scheme, q, backend="gloo", NB=NB, gpu_per_rank=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    gpu = rank if gpu_per_rank else 0
     if backend == "nccl":
-        torch.cuda.set_device(0)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda:0"))
+        torch.cuda.set_device(gpu)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", gpu))
     else:
         dist.init_process_group("gloo", rank=rank, world_size=world)
     host_t = (lambda t: t.cpu()) if backend == "gloo" else (lambda t: t)  # RCCL moves device tensors
@@ -41,8 +42,8 @@ def _worker(rank, world, port, scheme, q, backend="gloo", NB=NB):
                                              scatter_stream, unpack_device)
         from oracle import oracle as O
 
-        torch.cuda.set_device(0)
-        codec = BlockCodec(device="cuda:0")
+        torch.cuda.set_device(gpu)
+        codec = BlockCodec(device=f"cuda:{gpu}")
         n_glob = NB * BS - TAIL
         raw = codec.generate(0, 0.155, 0x5EED0004, n_glob)
         mine = list(rank_blocks(NB, rank, world, scheme))
@@ -69,7 +70,7 @@ def _worker(rank, world, port, scheme, q, backend="gloo", NB=NB):
         cb2 = {"n_total": local.numel(), "out": slots, "comp_len": my_lens.cuda(), "sidecar": my_side.cuda()}
         for use_side in (True, False):
             out = torch.full_like(local, 0xA5)
-            st = torch.full((nb,), -99, dtype=torch.int32, device="cuda:0")
+            st = torch.full((nb,), -99, dtype=torch.int32, device=f"cuda:{gpu}")
             codec.decompress_into(cb2, out, st, use_sidecar=use_side)
             torch.cuda.synchronize()
             ok &= int(st.abs().max()) == 0 and bool(torch.equal(out, local))
@@ -83,7 +84,7 @@ def _worker(rank, world, port, scheme, q, backend="gloo", NB=NB):
             hsel = select_blocks(g_stream.cpu(), offs, g_lens.cpu(), sel)
             ok &= bool(torch.equal(dsel.cpu(), hsel))
     finally:
-        flag = torch.tensor([1 if ok else 0], device="cpu" if backend == "gloo" else "cuda:0")
+        flag = torch.tensor([1 if ok else 0], device="cpu" if backend == "gloo" else f"cuda:{gpu}")
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         if rank == 0:
             q.put(bool(flag.item()))
@@ -216,3 +217,52 @@ def test_bench_two_ranks_exchange_ok():
     assert len(lines) == 1
     line = json.loads(lines[0])
     assert line["c4_exchange"]["verified"] is True and line["verified_roundtrip"] is True
+
+
+def _two_gpus():
+    return torch.cuda.device_count() >= 2
+
+
+@pytest.mark.skipif(not _two_gpus(), reason="needs two GPUs (one RCCL rank per GPU)")
+@pytest.mark.parametrize("scheme", ["contiguous", "round_robin"])
+def test_rccl_two_gpus_encode_gather_scatter_decode(scheme):
+    """The first real multi-GPU exchange: two ranks on two GPUs over RCCL
+    (nccl backend, one rank per device), the same shard -> encode -> gatherv
+    -> oracle bytes -> scatter -> decode path as above."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, scheme, q, "nccl", NB, True)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert q.get(timeout=10) is True
+
+
+@pytest.mark.skipif(not _two_gpus(), reason="needs two GPUs (one RCCL rank per GPU)")
+def test_bench_rccl_two_gpus():
+    """bench.py --gpus 2 as the driver's SCALE run launches it (self-launched
+    ranks, RCCL, one GPU each), on 256 MiB per GPU: one line with n_gpus 2,
+    the step verified, the C4 exchange verified over RCCL with its gather
+    priced against the xGMI ingress roof (gather_roof_frac present)."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.pop("FSEHIP_BENCH_BACKEND", None)
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--bytes", str(256 << 20), "--no-cpu", "--gather-timeout", "120"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=400)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    assert len(lines) == 1, r.stdout[-2000:]
+    line = json.loads(lines[0])
+    print(json.dumps({k: line[k] for k in ("value", "n_gpus", "scaling", "ms_per_step")}))
+    print(json.dumps(line["c4_exchange"]))
+    assert line["n_gpus"] == 2 and line["verified_roundtrip"] is True
+    c4 = line["c4_exchange"]
+    assert c4["verified"] is True and c4["backend"] == "nccl" and c4["gather_roof_frac"] is not None

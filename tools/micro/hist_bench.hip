@@ -112,6 +112,74 @@ __global__ __launch_bounds__(64) void hist_kernel_v5(const uint8_t* __restrict__
     out[(uint64_t)blockIdx.x * 256 + 4 * lane + 3] = acc_hi >> 16;
 }
 
+
+// Round 6 (verdict r05 item 5: skewed data's same-address atomics).  All on
+// the product layout V2 (16 u16 copies [bin][sub], word (lane / 2) % 8, half
+// lane % 2):
+//  V6: the product's loop as is (reference for the two below)
+//  V7: a wave-uniform hot symbol (the block's first byte): lanes whose byte is
+//      the hot symbol skip the atomic (exec-masked off) and the wave counts
+//      them with a ballot popcount in a scalar register
+//  V8: run aggregation per lane: a byte equal to the lane's previous byte
+//      only extends the run; a different byte flushes the run with one
+//      atomic (exec-masked to the flushing lanes)
+template <int V>
+__global__ __launch_bounds__(64) void hist_kernel_r6(const uint8_t* __restrict__ src, uint32_t* __restrict__ out) {
+    __shared__ uint32_t h[8 * 256];
+    const uint32_t lane = threadIdx.x;
+    for (uint32_t i = lane; i < 8 * 256; i += 64) h[i] = 0;
+    __syncthreads();
+    const uint8_t* blk = src + (uint64_t)blockIdx.x * BS;
+    const uint4* v4 = reinterpret_cast<const uint4*>(blk);
+    uint32_t* mine = h + ((lane >> 1) & 7u);
+    const uint32_t inc = 1u << (16u * (lane & 1u));
+    const uint32_t hot = __builtin_amdgcn_readfirstlane((uint32_t)blk[0]);
+    uint32_t hot_cnt = 0;        // V7: wave-uniform
+    uint32_t cur = 0x100u, run = 0;  // V8: per lane
+    auto add = [&](uint32_t b) {
+        if (V == 6) atomicAdd(&mine[b * 8u], inc);
+        if (V == 7) {
+            const bool is_hot = b == hot;
+            hot_cnt += (uint32_t)__popcll(__ballot(is_hot));
+            if (!is_hot) atomicAdd(&mine[b * 8u], inc);
+        }
+        if (V == 8) {
+            if (b == cur) {
+                run += 1u;
+            } else {
+                if (run) atomicAdd(&mine[cur * 8u], run << (16u * (lane & 1u)));
+                cur = b;
+                run = 1u;
+            }
+        }
+    };
+    constexpr uint32_t U = 8;
+    for (uint32_t v = 0; v < BS / 16; v += U * 64) {
+        uint4 d[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) d[u] = v4[v + u * 64 + lane];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint32_t w[4] = {d[u].x, d[u].y, d[u].z, d[u].w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) add((w[k] >> (8 * b)) & 0xFFu);
+        }
+    }
+    if (V == 8 && run) atomicAdd(&mine[cur * 8u], run << (16u * (lane & 1u)));
+    __syncthreads();
+    for (uint32_t s = lane; s < 256; s += 64) {
+        uint32_t c = 0;
+        for (int q = 0; q < 8; ++q) {
+            const uint32_t x = h[s * 8 + q];
+            c += (x & 0xFFFFu) + (x >> 16);
+        }
+        if (V == 7 && s == hot) c += hot_cnt;  // wave-uniform count of the skipped bytes
+        out[(uint64_t)blockIdx.x * 256 + s] = c;
+    }
+}
+
 template <int V>
 int run(const uint8_t* d_src, uint32_t* d_out, uint32_t nb, std::vector<uint32_t>& ref, const char* name) {
     hipEvent_t a, b;
@@ -119,7 +187,8 @@ int run(const uint8_t* d_src, uint32_t* d_out, uint32_t nb, std::vector<uint32_t
     CK(hipEventCreate(&b));
     auto launch = [&]() {
         if (V == 5) hipLaunchKernelGGL(hist_kernel_v5, dim3(nb), dim3(64), 0, 0, d_src, d_out);
-        else hipLaunchKernelGGL(hist_kernel<V == 5 ? 0 : V>, dim3(nb), dim3(64), 0, 0, d_src, d_out);
+        else if (V >= 6) hipLaunchKernelGGL(hist_kernel_r6<V>, dim3(nb), dim3(64), 0, 0, d_src, d_out);
+        else hipLaunchKernelGGL(hist_kernel<V>, dim3(nb), dim3(64), 0, 0, d_src, d_out);
     };
     launch();
     CK(hipDeviceSynchronize());
@@ -158,5 +227,8 @@ int main(int argc, char** argv) {
     run<3>(d_src, d_out, nb, ref, "V3 8x257 [sub][bin]");
     run<4>(d_src, d_out, nb, ref, "V4 16x257 [sub][bin]");
     run<5>(d_src, d_out, nb, ref, "V5 per-lane u8 [q][lane] + flush");
+    run<6>(d_src, d_out, nb, ref, "V6 product loop (16 u16)");
+    run<7>(d_src, d_out, nb, ref, "V7 hot symbol by ballot");
+    run<8>(d_src, d_out, nb, ref, "V8 per-lane runs");
     return 0;
 }
