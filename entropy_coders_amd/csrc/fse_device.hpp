@@ -152,9 +152,12 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const u32x4 gbl_u4;
 typedef __attribute__((address_space(1))) const uint8_t gbl_u8;
 
+#ifndef FSEHIP_HIST_HOT
+#define FSEHIP_HIST_HOT 0
+#endif
 template <uint32_t HS>
-__device__ __attribute__((noinline)) void wave_histogram_seg(const uint8_t* __restrict__ src_generic, uint32_t n,
-                                                             uint32_t* hs_generic) {
+__device__ __attribute__((noinline)) uint32_t wave_histogram_seg(const uint8_t* __restrict__ src_generic, uint32_t n,
+                                                                 uint32_t* hs_generic) {
     static_assert(HS == 8 || HS == 16, "sub-histograms");
     constexpr uint32_t WPB = hist_words<HS>() / 256u;  // words per bin
     const uint32_t lane = lane_id();
@@ -162,7 +165,14 @@ __device__ __attribute__((noinline)) void wave_histogram_seg(const uint8_t* __re
     lds_u32* mine = (lds_u32*)hs_generic + (HIST_U16 ? ((lane >> 1) & (HS / 2u - 1u)) : (lane & (HS - 1u)));
     const uint32_t inc = HIST_U16 ? 1u << (16u * (lane & 1u)) : 1u;
     gbl_u8* src = (gbl_u8*)src_generic;
+    const uint32_t hot = FSEHIP_HIST_HOT && n ? __builtin_amdgcn_readfirstlane((uint32_t)src[0]) : 0x100u;
+    uint32_t hot_cnt = 0;
     auto add = [&](uint32_t byte) {
+        if (FSEHIP_HIST_HOT) {
+            const bool h = byte == hot;
+            hot_cnt += (uint32_t)__popcll(__ballot(h));
+            if (h) return;
+        }
         __hip_atomic_fetch_add(&mine[byte * WPB], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
     uint32_t done = 0;
@@ -210,7 +220,11 @@ __device__ __attribute__((noinline)) void wave_histogram_seg(const uint8_t* __re
         }
         done = nvec << 4;
     }
-    for (uint32_t i = done + lane; i < n; i += WAVE) add(src[i]);
+    for (uint32_t i = done + lane; i < n; i += WAVE) {
+        const uint32_t byte = src[i];
+        __hip_atomic_fetch_add(&mine[byte * WPB], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    return FSEHIP_HIST_HOT ? (hot_cnt << 8) | (hot & 0xFFu) : 0u;
 }
 
 template <uint32_t HS = HSUB>
@@ -224,8 +238,9 @@ __device__ inline uint32_t wave_histogram(const uint8_t* __restrict__ src, uint3
         for (uint32_t i = lane; i < NW; i += WAVE) hs[i] = 0;
         wave_sync();
         const uint32_t m = min(n - seg, HIST_SEG);
-        wave_histogram_seg<HS>(src + seg, m, hs);
+        const uint32_t hot = wave_histogram_seg<HS>(src + seg, m, hs);
         wave_sync();
+        if (lane == 0 && (hot >> 8)) counts[hot & 0xFFu] += hot >> 8;
         for (uint32_t s = lane; s < 256; s += WAVE) {
             uint32_t c = 0;
 #pragma unroll

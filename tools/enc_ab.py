@@ -19,6 +19,8 @@ n = 1 << 30
 cases = [("C2", 0, 0.155, 0)]
 if os.environ.get("AB_WIDE") == "1":
     cases += [("geometric", 1, 0.5, 0), ("skewed L11", 0, 0.77, 11), ("skewed L12", 0, 0.77, 12)]
+if os.environ.get("AB_WIDE") == "2":  # the histogram's cases: skewed (C5) and near-uniform data at L = 9
+    cases += [("skewed L9", 0, 0.77, 9), ("skewed L10", 0, 0.77, 10), ("uniform L9", 2, 0.0, 9)]
 out = []
 for name, kind, prob, tlog in cases:
     codec = BlockCodec(table_log=tlog)

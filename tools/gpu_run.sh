@@ -18,6 +18,9 @@
 #   traffic            FETCH_SIZE and WRITE_SIZE passes (tools/pmc_summary.py)
 #   fuzz[:CASES[:SEED]] the randomized oracle sweep (tests/test_gpu_fuzz.py)
 #   micro:NAME[:ARGS]  a prebuilt probe under tools/micro/
+#   ab:V1,V2,...       encode A/B (tools/enc_ab.py, AB_WIDE from the environment) of library
+#                      builds libfsehip_V.so ("product" = libfsehip.so), three alternating
+#                      rounds, C2 bytes checked against the first build's digest
 #
 # Variant libraries (FSEHIP_LIB=libfsehip_NAME.so) are selected by the caller's
 # environment: FSEHIP_LIB=libfsehip_diag.so tools/gpu_run.sh OUT bench ...
@@ -27,7 +30,7 @@ O=gpurun_out/${1:?usage: tools/gpu_run.sh OUT STEP...}
 shift
 mkdir -p "$O"
 export TMPDIR=/tmp
-nb=0; np=0
+nb=0; np=0; nm=0
 fail() { echo "step '$1' failed (rc $2): stopping"; tail -30 "$3"; exit "$2"; }
 for step in "$@"; do
   name=${step%%:*}
@@ -71,9 +74,19 @@ for step in "$@"; do
         > "$O/pytest_fuzz.log" 2>&1 || fail "$step" $? "$O/pytest_fuzz.log"
       tail -1 "$O/pytest_fuzz.log" ;;
     micro)
+      nm=$((nm + 1))
       prog=${arg%%:*}; margs=""; [[ "$arg" == *:* ]] && margs=${arg#*:}
-      timeout -k 10 300 "./tools/micro/$prog" ${margs//,/ } > "$O/$prog.txt" 2>&1 || fail "$step" $? "$O/$prog.txt"
-      tail -5 "$O/$prog.txt" ;;
+      timeout -k 10 300 "./tools/micro/$prog" ${margs//,/ } > "$O/${prog}_$nm.txt" 2>&1 || fail "$step" $? "$O/${prog}_$nm.txt"
+      echo "$prog ${margs//,/ }"; tail -12 "$O/${prog}_$nm.txt" ;;
+    ab)
+      for r in 1 2 3; do
+        for v in ${arg//,/ }; do
+          lib=libfsehip_$v.so; [ "$v" = product ] && lib=libfsehip.so
+          FSEHIP_LIB=$lib AB_DIGEST="$O/ab_digest" timeout -k 10 300 python3 tools/enc_ab.py >> "$O/ab.txt" 2>&1 \
+            || fail "$step" $? "$O/ab.txt"
+        done
+      done
+      cat "$O/ab.txt" ;;
     *)
       echo "unknown step '$step'"; exit 2 ;;
   esac
