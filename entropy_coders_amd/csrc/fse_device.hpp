@@ -138,8 +138,15 @@ constexpr uint32_t HSUB = FSE_HSUB;  // default sub-histogram count
 #define FSE_HIST_U16 1
 #endif
 constexpr bool HIST_U16 = FSE_HIST_U16 != 0;
+#ifndef FSEHIP_HIST_HOT
+#define FSEHIP_HIST_HOT 0
+#endif
+// hot_words: the hot symbol's own counters after the bins (two lanes per word;
+// the 16-copy layout of one block per wave only)
 template <uint32_t HS>
-constexpr uint32_t hist_words() { return HIST_U16 ? 256 * HS / 2 : 256 * HS; }
+constexpr uint32_t hot_words() { return FSEHIP_HIST_HOT && HS == 16 ? 32u : 0u; }
+template <uint32_t HS>
+constexpr uint32_t hist_words() { return (HIST_U16 ? 256 * HS / 2 : 256 * HS) + hot_words<HS>(); }
 constexpr uint32_t HIST_WORDS = hist_words<HSUB>();
 constexpr uint32_t HIST_SEG = 1u << 18;
 
@@ -152,28 +159,27 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const u32x4 gbl_u4;
 typedef __attribute__((address_space(1))) const uint8_t gbl_u8;
 
-#ifndef FSEHIP_HIST_HOT
-#define FSEHIP_HIST_HOT 0
-#endif
 template <uint32_t HS>
-__device__ __attribute__((noinline)) uint32_t wave_histogram_seg(const uint8_t* __restrict__ src_generic, uint32_t n,
-                                                                 uint32_t* hs_generic) {
+__device__ __attribute__((noinline)) void wave_histogram_seg(const uint8_t* __restrict__ src_generic, uint32_t n,
+                                                             uint32_t* hs_generic) {
     static_assert(HS == 8 || HS == 16, "sub-histograms");
-    constexpr uint32_t WPB = hist_words<HS>() / 256u;  // words per bin
+    constexpr bool HOT = hot_words<HS>() != 0;
+    static_assert(HIST_U16 || !HOT, "hot words hold two u16 halves");
+    constexpr uint32_t WPB = (hist_words<HS>() - hot_words<HS>()) / 256u;  // words per bin
     const uint32_t lane = lane_id();
     // byte address of this lane's copy: ((lane / 2) % (HS / 2)) words into each bin's
     lds_u32* mine = (lds_u32*)hs_generic + (HIST_U16 ? ((lane >> 1) & (HS / 2u - 1u)) : (lane & (HS - 1u)));
     const uint32_t inc = HIST_U16 ? 1u << (16u * (lane & 1u)) : 1u;
     gbl_u8* src = (gbl_u8*)src_generic;
-    const uint32_t hot = FSEHIP_HIST_HOT && n ? __builtin_amdgcn_readfirstlane((uint32_t)src[0]) : 0x100u;
-    uint32_t hot_cnt = 0;
+    // The hot symbol (the segment's first byte, wave-uniform) counts in words
+    // of its own, two lanes per word, instead of its bin's 8 words shared by
+    // 8 lanes each: a skewed block's dominant-symbol atomics stop queueing on
+    // the same addresses.  One compare and one select per byte, no branch.
+    const uint32_t hot = HOT && n ? __builtin_amdgcn_readfirstlane((uint32_t)src[0]) : 0x100u;
+    lds_u32* hot_word = (lds_u32*)hs_generic + 256u * WPB + (lane >> 1);
     auto add = [&](uint32_t byte) {
-        if (FSEHIP_HIST_HOT) {
-            const bool h = byte == hot;
-            hot_cnt += (uint32_t)__popcll(__ballot(h));
-            if (h) return;
-        }
-        __hip_atomic_fetch_add(&mine[byte * WPB], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        lds_u32* a = (HOT && byte == hot) ? hot_word : &mine[byte * WPB];
+        __hip_atomic_fetch_add(a, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
     uint32_t done = 0;
     if ((reinterpret_cast<uintptr_t>(src_generic) & 15u) == 0) {
@@ -220,17 +226,13 @@ __device__ __attribute__((noinline)) uint32_t wave_histogram_seg(const uint8_t* 
         }
         done = nvec << 4;
     }
-    for (uint32_t i = done + lane; i < n; i += WAVE) {
-        const uint32_t byte = src[i];
-        __hip_atomic_fetch_add(&mine[byte * WPB], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    return FSEHIP_HIST_HOT ? (hot_cnt << 8) | (hot & 0xFFu) : 0u;
+    for (uint32_t i = done + lane; i < n; i += WAVE) add(src[i]);
 }
 
 template <uint32_t HS = HSUB>
 __device__ inline uint32_t wave_histogram(const uint8_t* __restrict__ src, uint32_t n,
                                           uint32_t* hs /*LDS [hist_words<HS>()]*/, uint32_t* counts /*LDS[256]*/) {
-    constexpr uint32_t NW = hist_words<HS>(), Q = NW / 256u / 4u;  // uint4 per bin
+    constexpr uint32_t HW = hot_words<HS>(), NW = hist_words<HS>(), Q = (NW - HW) / 256u / 4u;  // uint4 per bin
     const uint32_t lane = lane_id();
     for (uint32_t s = lane; s < 256; s += WAVE) counts[s] = 0;
     uint32_t seg = 0;
@@ -238,9 +240,13 @@ __device__ inline uint32_t wave_histogram(const uint8_t* __restrict__ src, uint3
         for (uint32_t i = lane; i < NW; i += WAVE) hs[i] = 0;
         wave_sync();
         const uint32_t m = min(n - seg, HIST_SEG);
-        const uint32_t hot = wave_histogram_seg<HS>(src + seg, m, hs);
+        wave_histogram_seg<HS>(src + seg, m, hs);
         wave_sync();
-        if (lane == 0 && (hot >> 8)) counts[hot & 0xFFu] += hot >> 8;
+        if (HW) {  // the hot symbol's own words
+            const uint32_t x = lane < HW ? hs[NW - HW + lane] : 0u;
+            const uint32_t t = bcast63(wave_incl_sum((x & 0xFFFFu) + (x >> 16)));
+            if (lane == 0 && m) counts[src[seg]] += t;
+        }
         for (uint32_t s = lane; s < 256; s += WAVE) {
             uint32_t c = 0;
 #pragma unroll
