@@ -177,8 +177,11 @@ __device__ __attribute__((noinline)) void wave_histogram_seg(const uint8_t* __re
     // the same addresses.  One compare and one select per byte, no branch.
     const uint32_t hot = HOT && n ? __builtin_amdgcn_readfirstlane((uint32_t)src[0]) : 0x100u;
     lds_u32* hot_word = (lds_u32*)hs_generic + 256u * WPB + (lane >> 1);
-    auto add = [&](uint32_t byte) {
-        lds_u32* a = (HOT && byte == hot) ? hot_word : &mine[byte * WPB];
+    auto add_plain = [&](uint32_t byte) {
+        __hip_atomic_fetch_add(&mine[byte * WPB], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    auto add_hot = [&](uint32_t byte) {
+        lds_u32* a = byte == hot ? hot_word : &mine[byte * WPB];
         __hip_atomic_fetch_add(a, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
     uint32_t done = 0;
@@ -189,10 +192,36 @@ __device__ __attribute__((noinline)) void wave_histogram_seg(const uint8_t* __re
         const uint32_t nvec = n >> 4;
         gbl_u4* v4 = (gbl_u4*)src_generic;
         uint32_t v = 0;
-        auto count = [&](const u32x4* d) {
+        auto batches = [&](auto add) {
+            auto count = [&](const u32x4* d) {
 #pragma unroll
-            for (uint32_t u = 0; u < U; ++u) {
-                const uint32_t w[4] = {d[u].x, d[u].y, d[u].z, d[u].w};
+                for (uint32_t u = 0; u < U; ++u) {
+                    const uint32_t w[4] = {d[u].x, d[u].y, d[u].z, d[u].w};
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+                        for (int b = 0; b < 4; ++b) add((w[k] >> (8 * b)) & 0xFFu);
+                    }
+                }
+            };
+            if (U * WAVE <= nvec) {
+                u32x4 d[U];
+#pragma unroll
+                for (uint32_t u = 0; u < U; ++u) d[u] = v4[u * WAVE + lane];
+                for (; v + 2u * U * WAVE <= nvec; v += U * WAVE) {
+                    u32x4 e[U];
+#pragma unroll
+                    for (uint32_t u = 0; u < U; ++u) e[u] = v4[v + U * WAVE + u * WAVE + lane];
+                    count(d);
+#pragma unroll
+                    for (uint32_t u = 0; u < U; ++u) d[u] = e[u];
+                }
+                count(d);
+                v += U * WAVE;
+            }
+            for (v += lane; v < nvec; v += WAVE) {
+                const u32x4 d = v4[v];
+                const uint32_t w[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
 #pragma unroll
@@ -200,33 +229,25 @@ __device__ __attribute__((noinline)) void wave_histogram_seg(const uint8_t* __re
                 }
             }
         };
-        if (U * WAVE <= nvec) {
-            u32x4 d[U];
+        // a block takes the hot path when at least half of a 1 KiB sample
+        // (each lane's first 16 bytes) is the hot symbol; the others keep the
+        // plain loop, with no per-byte compare
+        bool skew = false;
+        if (HOT && nvec >= WAVE) {
+            const u32x4 q = v4[lane];
+            const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+            uint32_t c = 0;
 #pragma unroll
-            for (uint32_t u = 0; u < U; ++u) d[u] = v4[u * WAVE + lane];
-            for (; v + 2u * U * WAVE <= nvec; v += U * WAVE) {
-                u32x4 e[U];
+            for (int k = 0; k < 4; ++k)
 #pragma unroll
-                for (uint32_t u = 0; u < U; ++u) e[u] = v4[v + U * WAVE + u * WAVE + lane];
-                count(d);
-#pragma unroll
-                for (uint32_t u = 0; u < U; ++u) d[u] = e[u];
-            }
-            count(d);
-            v += U * WAVE;
+                for (int b = 0; b < 4; ++b) c += ((w[k] >> (8 * b)) & 0xFFu) == hot ? 1u : 0u;
+            skew = bcast63(wave_incl_sum(c)) >= 8u * WAVE;
         }
-        for (v += lane; v < nvec; v += WAVE) {
-            const u32x4 d = v4[v];
-            const uint32_t w[4] = {d.x, d.y, d.z, d.w};
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-#pragma unroll
-                for (int b = 0; b < 4; ++b) add((w[k] >> (8 * b)) & 0xFFu);
-            }
-        }
+        if (skew) batches(add_hot);
+        else batches(add_plain);
         done = nvec << 4;
     }
-    for (uint32_t i = done + lane; i < n; i += WAVE) add(src[i]);
+    for (uint32_t i = done + lane; i < n; i += WAVE) add_plain(src[i]);
 }
 
 template <uint32_t HS = HSUB>

@@ -21,6 +21,8 @@
 #   ab:V1,V2,...       encode A/B (tools/enc_ab.py, AB_WIDE from the environment) of library
 #                      builds libfsehip_V.so ("product" = libfsehip.so), three alternating
 #                      rounds, C2 bytes checked against the first build's digest
+#   abdec:V1,V2,...    decode A/B (tools/time_dec.py: C3, C2 encode / decode, exactness),
+#                      three alternating rounds
 #
 # Variant libraries (FSEHIP_LIB=libfsehip_NAME.so) are selected by the caller's
 # environment: FSEHIP_LIB=libfsehip_diag.so tools/gpu_run.sh OUT bench ...
@@ -87,6 +89,14 @@ for step in "$@"; do
         done
       done
       cat "$O/ab.txt" ;;
+    abdec)
+      for r in 1 2 3; do
+        for v in ${arg//,/ }; do
+          lib=libfsehip_$v.so; [ "$v" = product ] && lib=libfsehip.so
+          FSEHIP_LIB=$lib timeout -k 10 300 python3 tools/time_dec.py >> "$O/abdec.txt" 2>&1 || fail "$step" $? "$O/abdec.txt"
+        done
+      done
+      grep '^{' "$O/abdec.txt" ;;
     *)
       echo "unknown step '$step'"; exit 2 ;;
   esac
