@@ -237,18 +237,10 @@ struct LdsChain {
     }
     __device__ __forceinline__ uint32_t pair(const uint32_t* pay, const uint8_t* dtb) {
         const int32_t lo = (pos - PAIR_MAX_BITS) & ~31;
-#if FSEHIP_DEC_W2
-        // both window words in one ds_read2_b32: no word select, no carried words
-        const uint32_t* wp = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(pay) + (lo >> 3));
-        const uint32_t w0 = wp[0], w1 = wp[1];
-        const uint32_t e0 = *reinterpret_cast<const uint32_t*>(dtb + a0);
-        const uint32_t e1 = *reinterpret_cast<const uint32_t*>(dtb + a1);
-#else
         const uint32_t w0 = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(pay) + (lo >> 3));
         const uint32_t e0 = *reinterpret_cast<const uint32_t*>(dtb + a0);
         const uint32_t e1 = *reinterpret_cast<const uint32_t*>(dtb + a1);
         const uint32_t w1 = lo == B ? whi : wlo;
-#endif
         pos -= (int32_t)((e0 + e1) & 0xFFu);
         const uint32_t x = (uint32_t)((((uint64_t)w1 << 32) | w0) >> (uint32_t)(pos - lo));
         B = lo;

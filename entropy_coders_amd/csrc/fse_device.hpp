@@ -138,13 +138,10 @@ constexpr uint32_t HSUB = FSE_HSUB;  // default sub-histogram count
 #define FSE_HIST_U16 1
 #endif
 constexpr bool HIST_U16 = FSE_HIST_U16 != 0;
-#ifndef FSEHIP_HIST_HOT
-#define FSEHIP_HIST_HOT 0
-#endif
 // hot_words: the hot symbol's own counters after the bins (two lanes per word;
 // the 16-copy layout of one block per wave only)
 template <uint32_t HS>
-constexpr uint32_t hot_words() { return FSEHIP_HIST_HOT && HS == 16 ? 32u : 0u; }
+constexpr uint32_t hot_words() { return HS == 16 ? 32u : 0u; }
 template <uint32_t HS>
 constexpr uint32_t hist_words() { return (HIST_U16 ? 256 * HS / 2 : 256 * HS) + hot_words<HS>(); }
 constexpr uint32_t HIST_WORDS = hist_words<HSUB>();

@@ -96,8 +96,8 @@ def _find(meta, prefix):
 
 # (kernel, LDS bytes today, workgroups per CU it must keep)
 GUARDS = [
-    ("_ZN6fsehip20encode_blocks_kernelILi11ELi64ELi2EE", 14640, 11),   # C2 encode (fse_compress2, L <= 11)
-    ("_ZN6fsehip20encode_blocks_kernelILi11ELi64ELi1EE", 14640, 11),   # 1-state encode
+    ("_ZN6fsehip20encode_blocks_kernelILi11ELi64ELi2EE", 14768, 11),   # C2 encode (fse_compress2, L <= 11)
+    ("_ZN6fsehip20encode_blocks_kernelILi11ELi64ELi1EE", 14768, 11),   # 1-state encode
     ("_ZN6fsehip17decode_pre_kernelILi11ELj45056ELi2ELi1ELj512EE", 53296, 3),  # C2/C3 segment decode
     ("_ZN6fsehip17decode_pre_kernelILi11ELj45056ELi2ELi1ELj256EE", 53280, 3),  # 128-pair checkpoints
     ("_ZN6fsehip20dtable_blocks_kernelILi11EE", 7680, 21),             # decode tables

@@ -57,9 +57,16 @@ def main():
         out[name] = row
         print(name, json.dumps(row))
     if "--json" in sys.argv:
-        with open(sys.argv[sys.argv.index("--json") + 1], "w") as fh:
-            json.dump({"source": "rocprofv3 --pmc SQ passes (tools/pmc_sq.sh) over tools/prof_bench.py, last launch "
-                                 "of each kind; tools/lds_summary.py", "cus": CUS, "kernels": out}, fh, indent=1)
+        path = sys.argv[sys.argv.index("--json") + 1]
+        if os.path.exists(path):  # keep the probe-derived splits (tools/lds_split*.py) of the kernels
+            old = json.load(open(path)).get("kernels", {})
+            for name, row in out.items():
+                if "split" in old.get(name, {}):
+                    row["split"] = old[name]["split"]
+        with open(path, "w") as fh:
+            json.dump({"source": "rocprofv3 --pmc SQ pass (tools/gpu_run.sh pmc:SQ_LDS_IDX_ACTIVE,...) over "
+                                 "tools/prof_bench.py, last launch of each kind; tools/lds_summary.py",
+                       "cus": CUS, "kernels": out}, fh, indent=1)
 
 
 if __name__ == "__main__":
