@@ -434,7 +434,7 @@ def load_traffic(name: str):
 def roofline_lds(kernel: str, ms: float, profiled: bool = True, alg_bytes: int = 0):
     """LDS-side roofline of a kernel whose launch took `ms` (HIP events, this
     run): its LDS-array cycles per launch summed over the CUs (rocprofv3
-    SQ_LDS_IDX_ACTIVE, profiles/lds.json from tools/lds_pass.sh +
+    SQ_LDS_IDX_ACTIVE, profiles/lds.json from the tools/gpu_run.sh pmc: pass +
     tools/lds_summary.py, same workload) per CU-cycle of this launch, at the
     clock measured in the profiled launch, against the LDS's peak of one
     array cycle per clock (MI355X_MICROARCH.md §LDS).  Conflict cycles are
@@ -458,7 +458,7 @@ def roofline_lds(kernel: str, ms: float, profiled: bool = True, alg_bytes: int =
            "conflict_share": round(k["bank_conflict_cycles_per_launch"] / max(k["lds_array_cycles_per_launch"], 1), 4),
            "lds_array_cycles_per_launch": k["lds_array_cycles_per_launch"], "clock_ghz": clk,
            "source": "profiles/lds.json: rocprofv3 SQ_LDS_IDX_ACTIVE / SQ_LDS_BANK_CONFLICT / GRBM_GUI_ACTIVE per "
-                     "launch (tools/lds_pass.sh, tools/lds_summary.py); time = this run's HIP events"}
+                     "launch (tools/gpu_run.sh pmc:, tools/lds_summary.py); time = this run's HIP events"}
     # the launch can take no less than its LDS-array cycles at one per CU-cycle:
     # the HBM-roofline fraction this design could reach with the LDS 100 % busy
     min_ms = k["lds_array_cycles_per_launch"] / (doc.get("cus", 256) * clk * 1e9) * 1e3
@@ -478,7 +478,7 @@ def roofline(kernel: str, ms: float, alg_bytes: int, what: str, profiled: bool =
     return {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(kernel) if profiled else None,
             "traffic_source": "profiles/traffic.json: rocprofv3 FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, "
-                              "per launch (tools/traffic.sh, tools/pmc_summary.py)",
+                              "per launch (tools/gpu_run.sh traffic, tools/pmc_summary.py)",
             "algorithmic_bytes_per_launch": alg_bytes, "timed": what}
 
 

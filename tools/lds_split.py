@@ -1,6 +1,6 @@
 """Split the segment decoder's LDS-array cycles per 64-lane pair step into
 its table gathers and its payload read (verdict r04 item 3), from three
-counter passes (tools/lds_pass.sh + tools/lds_summary.py) over the same
+counter passes (tools/gpu_run.sh pmc: + tools/lds_summary.py) over the same
 workload: the product and two one-read probes built with
 tools/variant_build.sh --
   FSEHIP_ABL=256: one more random table-like gather per pair (an extra

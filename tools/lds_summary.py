@@ -1,4 +1,4 @@
-"""LDS-side roofline inputs from the SQ counter passes of tools/pmc_sq.sh
+"""LDS-side roofline inputs from the SQ counter passes of tools/gpu_run.sh pmc:
 (over tools/prof_bench.py): per fse kernel launch kind (last launch of each
 kind), the LDS-array cycles of one launch summed over the CUs
 (SQ_LDS_IDX_ACTIVE), the bank-conflict cycles among them

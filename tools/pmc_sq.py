@@ -1,4 +1,4 @@
-"""Summarise the SQ counter passes of tools/pmc_sq.sh (over
+"""Summarise the SQ counter passes of tools/gpu_run.sh pmc: (over
 tools/prof_bench.py) per fse kernel launch kind (last launch of each kind),
 with per-symbol ratios: VALU and LDS instructions per symbol (wave
 instructions x 64 lanes / raw bytes), LDS bank-conflict cycles as a fraction
@@ -54,7 +54,7 @@ def main():
         print(name, json.dumps({k: x for k, x in row.items() if not k.startswith("SQ_") and not k.startswith("GRBM")}))
     if "--json" in sys.argv:
         with open(sys.argv[sys.argv.index("--json") + 1], "w") as fh:
-            json.dump({"source": "rocprofv3 --pmc SQ passes (tools/pmc_sq.sh) over tools/prof_bench.py, "
+            json.dump({"source": "rocprofv3 --pmc SQ passes (tools/gpu_run.sh pmc:) over tools/prof_bench.py, "
                                  "last launch of each kind", "raw_bytes_per_launch": RAW, "kernels": out}, fh, indent=1)
 
 
