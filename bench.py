@@ -182,9 +182,13 @@ def forced_exchange_failure() -> str | None:
 def workload_name(args, n: int) -> str:
     fmt = "fse_compress2" if args.nstates == 2 else "fse_compress"
     gen = {0: "LUT", 1: "geometric", 2: "uniform"}.get(args.kind, f"kind {args.kind}")
-    c2 = (args.kind == 0 and args.prob == 0.155 and args.block == 65536 and n == 1 << 30)
-    tag = "C2" if c2 else "custom"
-    ent = " (H~4.02 bits/sym)" if c2 else ""
+    lut = args.kind == 0 and args.prob == 0.155 and args.block == 65536
+    c2 = lut and n == 1 << 30
+    # C4 (BASELINE configs[3]): 8 GiB in total, round-robin over the ranks
+    c4 = (lut and n == 8 << 30 and getattr(args, "strong", False) and args.scheme == "round_robin"
+          and args.gpus > 1)
+    tag = "C2" if c2 else "C4" if c4 else "custom"
+    ent = " (H~4.02 bits/sym)" if lut else ""
     where = "in total (strong scaling)" if getattr(args, "strong", False) else "per GPU"
     return (f"{tag}: {n / 2**30:g} GiB {where} as {-(-n // args.block)} x {args.block // 1024} KiB independent "
             f"blocks, {gen} generator p={args.prob}{ent}, encode ({fmt}-exact) + decode")
