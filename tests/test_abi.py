@@ -118,7 +118,7 @@ def test_product_library_reads_no_environment():
     assert not re.search(r"\bU (secure_)?getenv\b", dyn), "product library imports getenv"
     blob = open(path, "rb").read()
     for knob in (b"FSEHIP_DEBUG", b"FSEHIP_ENC_LANES", b"FSEHIP_SERIAL_DEFER", b"FSEHIP_SERIAL_DW",
-                 b"FSEHIP_STAMPS", b"FSEHIP_ENC_XLDS", b"FSEHIP_DT_XLDS"):
+                 b"FSEHIP_STAMPS", b"FSEHIP_ENC_XLDS", b"FSEHIP_DT_XLDS", b"FSEHIP_RANK_INJECT"):
         assert knob not in blob, knob
 
 

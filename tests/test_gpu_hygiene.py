@@ -60,7 +60,8 @@ def test_product_ignores_diagnostic_knobs(torch_cuda):
     FSEHIP_SERIAL_DW=2, the occupancy paddings): the product library still
     writes the oracle's bytes, sidecar and round trips."""
     env = dict(os.environ, PYTHONPATH=ROOT, FSEHIP_DEBUG="30", FSEHIP_ENC_LANES="32", FSEHIP_SERIAL_DEFER="0",
-               FSEHIP_SERIAL_DW="2", FSEHIP_ENC_XLDS="60000", FSEHIP_DT_XLDS="60000", FSEHIP_STAMPS="1")
+               FSEHIP_SERIAL_DW="2", FSEHIP_ENC_XLDS="60000", FSEHIP_DT_XLDS="60000", FSEHIP_STAMPS="1",
+               FSEHIP_RANK_INJECT="1")
     env.pop("FSEHIP_LIB", None)
     r = subprocess.run([sys.executable, "-c", _CHILD], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "child-ok" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
