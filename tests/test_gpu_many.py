@@ -132,6 +132,8 @@ def test_many_streams_log_classes(torch_cuda):
     bad = bytearray(comps[7])
     bad[0] = (bad[0] & 0xF0) | 0x0F  # log nibble 15: L = 20
     streams = comps[:100] + [c15] + comps[100:200] + [bytes(bad)] + [c12] + comps[200:]
+    # three of each large log too, so the L = 12 and L = 13..15 groups take the batch path
+    streams += [c15, c12, c15, c12, c15, c12]
     got = decompress2_many(streams, 65536)
     for i, (x, g) in enumerate(zip(streams, got)):
         try:
@@ -141,6 +143,7 @@ def test_many_streams_log_classes(torch_cuda):
             continue
         assert g == want, i
     assert got[100] == l15.tobytes() and got[202] == l12.tobytes()
+    assert got[-6:] == [l15.tobytes(), l12.tobytes()] * 3
 
 
 def test_many_rejects_bad_dst_and_nstates(torch_cuda):
