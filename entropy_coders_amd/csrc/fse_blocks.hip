@@ -159,7 +159,7 @@ __global__ __launch_bounds__(64) void table_kernel(const fse_norm_histogram* nh,
     const uint32_t size = 1u << L;
     int rc;
     if (enc) {
-        rc = wave_build_spread(
+        rc = wave_build_spread<64, true>(
             norm, L, tl, sym_at, occ, cumul, cnt,
             [&](uint32_t i, uint32_t s, uint32_t r) {
                 et->table[r] = (uint16_t)(size + i);  // fse.rs:157-162 (r = cumul[s] + rank)
@@ -188,7 +188,7 @@ __global__ __launch_bounds__(64) void table_kernel(const fse_norm_histogram* nh,
         }
         if (lane == 0) et->table_log = L;
     } else {
-        rc = wave_build_spread(norm, L, tl, sym_at, occ, cumul, cnt, [&](uint32_t i, uint32_t s, uint32_t r) {
+        rc = wave_build_spread<64, true>(norm, L, tl, sym_at, occ, cumul, cnt, [&](uint32_t i, uint32_t s, uint32_t r) {
             const uint32_t nx = r;  // symbol_next + rank (fse.rs:296-308, 329-331)
             const uint32_t nb = L - ilog2u(nx);
             fse_decode_transform e;

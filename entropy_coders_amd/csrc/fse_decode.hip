@@ -909,9 +909,9 @@ __global__ __launch_bounds__(64) void dtable_blocks_kernel(DtParams P) {
         // two-pass ranks need 2^L / 64 per-chunk registers: up to L = 12
         const RankAtomic ra{P.peer_ranks == 0u, occ, nullptr, 0u, &g_rank_fb_dec, P.rank_inject};
         if (LMAX <= 12)
-            rc = wave_build_spread<SIZE / 64u>(norm, L, tl, sym_at, occ, cumul, cnt, visit, first_x, ra, rk, pm,
+            rc = wave_build_spread<SIZE / 64u, true>(norm, L, tl, sym_at, occ, cumul, cnt, visit, first_x, ra, rk, pm,
                                                &P);
-        else rc = wave_build_spread(norm, L, tl, sym_at, occ, cumul, cnt, visit, first_x, ra);
+        else rc = wave_build_spread<64, true>(norm, L, tl, sym_at, occ, cumul, cnt, visit, first_x, ra);
     }
     FSE_STAMP(P, 8);
     if (lane == 0) P.dtinfo[gb] = rc == FSE_OK ? (int32_t)((uint32_t)hl | (L << 16)) : rc;

@@ -769,7 +769,9 @@ struct RankAtomic {
     uint32_t inject;      // diagnostics build only: chunk 0's ranks in descending lane order (fault injection)
 };
 
-template <uint32_t MAXCH = 64, typename Visit, typename Base, class SP = NoStamps>  // MAXCH: 2^LMAX / 64 chunks (two-pass ranks)
+// MAXCH: 2^LMAX / 64 chunks (two-pass ranks); INV: the atomic ranks' check in
+// inverse mode (RankAtomic::inv8), else in stateTable mode (RankAtomic::st)
+template <uint32_t MAXCH = 64, bool INV = false, typename Visit, typename Base, class SP = NoStamps>
 __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_t tl, uint8_t* sym_at,
                                         uint8_t* occ_sym, uint16_t* cumul, uint32_t* cnt, Visit visit, Base base,
                                         const RankAtomic& ra, uint16_t* RK = nullptr, uint64_t* PM = nullptr,
@@ -893,28 +895,32 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
         // records the lane that took it and whether it was the last slot its
         // chunk took for that symbol (the counter read back after the
         // instruction).
-        const bool inv = ra.inv8 != nullptr;
-        const uint32_t step = inv ? 0x10001u : 1u;
-        for (uint32_t s = lane; s < 256u; s += WAVE) cnt[s] = inv ? ((uint32_t)cumul[s] << 16) | base(s) : base(s);
+        constexpr uint32_t step = INV ? 0x10001u : 1u;
+        for (uint32_t s = lane; s < 256u; s += WAVE) cnt[s] = INV ? ((uint32_t)cumul[s] << 16) | base(s) : base(s);
         wave_sync();
+        // the next chunk's symbols are read while this chunk's atomics are in
+        // flight; in inverse mode the counter is read back right behind the
+        // atomic (a wave's LDS instructions run in order), one wait for both
+        uint32_t sy_next = lane < size ? sym_at[lane] : 0u;
         for (uint32_t i0 = 0; i0 < size; i0 += WAVE) {
             const uint32_t i = i0 + lane;
             const bool act = i < size;
-            const uint32_t sy = act ? sym_at[i] : 0u;
-            uint32_t r = 0;
-            if (act)
+            const uint32_t sy = sy_next;
+            if (i + WAVE < size) sy_next = sym_at[i + WAVE];
+            uint32_t r = 0, endw = 0;
+            if (act) {
                 r = __hip_atomic_fetch_add((lds_u32*)cnt + sy, step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (INV) endw = __hip_atomic_load((lds_u32*)cnt + sy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
             if (kDiag && ra.inject && i0 == 0) {  // fault injection: the lanes' order reversed
                 const uint64_t peers = match_key(sy, __ballot(act), key_bits(tl));
                 const uint32_t bl = (uint32_t)__popcll(peers & lanemask_lt()), k = (uint32_t)__popcll(peers);
                 r += (k - 1u - 2u * bl) * step;
             }
             if (act) {
-                if (inv) {
+                if (INV) {
                     const uint32_t g = r >> 16;
-                    const uint32_t end =
-                        __hip_atomic_load((lds_u32*)cnt + sy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >> 16;
-                    ra.inv8[g] = (uint8_t)(lane | (g + 1u == end ? 0x40u : 0u));
+                    ra.inv8[g] = (uint8_t)(lane | (g + 1u == (endw >> 16) ? 0x40u : 0u));
                     visit(i, sy, r & 0xFFFFu);
                 } else {
                     visit(i, sy, r);
@@ -926,7 +932,7 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
         // wave's instructions keep their order, so only lanes of one
         // instruction can be out of order, and only among themselves.
         bool bad = false;
-        if (inv) {
+        if (INV) {
             // consecutive slots g, g + 1 of one chunk's range for one symbol
             // (g not flagged last) must hold ascending lanes
             for (uint32_t q0 = 0; q0 < size; q0 += 8u * WAVE) {
