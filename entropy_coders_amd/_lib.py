@@ -124,6 +124,16 @@ def load() -> C.CDLL:
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"{LIB_PATH} is missing: build the HIP extension first "
                            "(make -C entropy_coders_amd); there is no CPU fallback")
+    # One HIP runtime per process: PyTorch ships its own libamdhip64.so.7 /
+    # libhsa-runtime64.so.1 and loads them by path; loaded first, the
+    # library's DT_NEEDED entries (same sonames) resolve to torch's copies.
+    # Loaded the other way round, /opt/rocm's runtime comes in first and torch
+    # then finds no GPU ("No HIP GPUs are available", seen when a test called
+    # the library before touching torch).  So torch, when installed, goes first.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(LIB_PATH)
     P, sz, u32, u64, i32 = C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint64, C.c_int32
     lib.fse_compress2.argtypes = [P, sz, P, sz, C.POINTER(sz), C.POINTER(u64)]
