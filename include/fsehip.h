@@ -84,8 +84,12 @@ int fse_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, s
  * UNSUPPORTED above 2^28 bytes; a null srcs[i] with src_lens[i] > 0 is
  * BAD_ARG).  Returns FSE_OK when the batch ran (look at statuses), or a
  * call-level error (BAD_ARG, NO_DEVICE, HIP).  Streams up to 4 MiB are
- * batched, in groups of at most 512 MiB of staging each way; longer ones
- * (and dst_stride above 128 MiB) take the single-stream path one by one.
+ * batched, grouped by the table log in their header (<= 11, 12, 13..15: each
+ * group runs the kernels and decode-table stride of its class, so one large
+ * or corrupt log does not move the others), in groups of at most 512 MiB of
+ * staging each way and 512 MiB of decode tables; longer streams, a log
+ * nibble above 15 (a header the crate rejects) and dst_stride above 128 MiB
+ * take the single-stream path one by one.
  *
  * Where the GPU pays.  A lone stream is one serial chain: fse_decompress2
  * takes ~1.4 ms per 64 KiB call on MI355X against ~0.14-0.4 ms on one host
