@@ -739,26 +739,23 @@ __global__ __launch_bounds__(NT) void decode_pre_kernel(DecParams P) {
     if constexpr (PASS <= 1) {
         decode_pre_block<LMAX, PMAX, NS, NT>(P, sm, blockIdx.x);
     } else {
-        __shared__ uint32_t dlist[NT];
-        __shared__ uint32_t dcnt[NW];
+        // the deferred blocks among this workgroup's NT candidates, as one
+        // ballot mask per wave (64 B of LDS instead of an NT-entry list: the
+        // L = 12 list pass fits 2 workgroups per CU with a 65,392-byte stage)
+        __shared__ uint64_t dmask[NW];
         const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
         const uint64_t G = gridDim.x;
         for (uint64_t r0 = blockIdx.x; r0 < P.n_blocks; r0 += G * NT) {
             const uint64_t gb = r0 + G * tid;
             const bool d = gb < P.n_blocks && P.status[gb] == FSE_DEFERRED;
             const uint64_t m = __ballot(d);
-            if (lane == 0) dcnt[wv] = (uint32_t)__popcll(m);
+            if (lane == 0) dmask[wv] = m;
             __syncthreads();
-            uint32_t base = 0, total = 0;
-#pragma unroll
             for (uint32_t w = 0; w < NW; ++w) {
-                base += w < wv ? dcnt[w] : 0u;
-                total += dcnt[w];
+                for (uint64_t mw = dmask[w]; mw; mw &= mw - 1u)  // workgroup-uniform
+                    decode_pre_block<LMAX, PMAX, NS, NT>(P, sm, r0 + G * (64u * w + (uint32_t)__builtin_ctzll(mw)));
             }
-            if (d) dlist[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = (uint32_t)gb;
-            __syncthreads();
-            for (uint32_t i = 0; i < total; ++i) decode_pre_block<LMAX, PMAX, NS, NT>(P, sm, dlist[i]);
-            __syncthreads();  // dlist / dcnt are rewritten by the next round
+            __syncthreads();  // dmask is rewritten by the next round
         }
     }
 }
@@ -2085,7 +2082,10 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
     // 66 KiB stage (2 per CU) for the deferred ones (near-uniform data,
     // ~65 KB).  Blocks above that use the windowed global-memory reader; at
     // L 13..15 (table 128 KiB) every block does.
-    constexpr uint32_t PP = 44u << 10, PB = 66u << 10;
+    // PB12: the L = 12 list pass's stage, the most that keeps 2 workgroups per
+    // CU beside its 16 KiB table (near-uniform blocks at L = 12, ~65.3 KB,
+    // fit; 1 per CU with a 66 KiB stage)
+    constexpr uint32_t PP = 44u << 10, PB = 66u << 10, PB12 = 65392u;
     static const uint32_t cus = [] {
         int dev = 0, n = 0;
         (void)hipGetDevice(&dev);
@@ -2116,7 +2116,7 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
             run(decode_pre_kernel<11, PB, 1, 2>, 2, 2);
         } else if (lmax <= 12) {
             run(decode_pre_kernel<12, PP - 8192, 1, 1>, 1, 0);
-            run(decode_pre_kernel<12, PB, 1, 2>, 2, 2);
+            run(decode_pre_kernel<12, PB12, 1, 2>, 2, 2);
         } else if (lmax <= 13) {
             run(decode_pre_kernel<13, PP, 1, 1>, 1, 0);
             run(decode_pre_kernel<13, PB, 1, 2>, 2, 1);
@@ -2135,10 +2135,10 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
             run(decode_pre_kernel<11, PB, 2, 2>, 2, 2);
         } else if (lmax <= 12 && wide) {
             run(decode_pre_kernel<12, PP - 8192, 2, 1, 512>, 1, 0, 512);
-            run(decode_pre_kernel<12, PB, 2, 2, 512>, 2, 2, 512);
+            run(decode_pre_kernel<12, PB12, 2, 2, 512>, 2, 2, 512);
         } else if (lmax <= 12) {
             run(decode_pre_kernel<12, PP - 8192, 2, 1>, 1, 0);
-            run(decode_pre_kernel<12, PB, 2, 2>, 2, 2);
+            run(decode_pre_kernel<12, PB12, 2, 2>, 2, 2);
         } else if (lmax <= 13 && wide) {  // 32 KiB table: 2 workgroups per CU, the list pass 1
             run(decode_pre_kernel<13, PP, 2, 1, 512>, 1, 0, 512);
             run(decode_pre_kernel<13, PB, 2, 2, 512>, 2, 1, 512);
