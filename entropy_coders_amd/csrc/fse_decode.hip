@@ -838,7 +838,9 @@ __global__ __launch_bounds__(64) void dtable_blocks_kernel(DtParams P) {
     // (the decoder's visit reads norm only); 7 KB per workgroup at L = 11
     __shared__ __attribute__((aligned(16))) uint16_t rk[SIZE];
     static_assert(SIZE + 256 * 4 + 256 * 2 <= SIZE * 2, "rank table must cover occ, cnt and cumul");
-    __shared__ uint64_t pm[64];  // rank peer masks (lds_peers)
+    // (no LDS peer masks: the peer-mask ranks run only when an atomic-rank
+    // table fails its check, and then match keys by ballot; the 512 B they
+    // took kept the kernel at 21 workgroups per CU instead of 22)
     uint8_t* occ = reinterpret_cast<uint8_t*>(rk);
     uint32_t* cnt = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(rk) + SIZE);
     uint16_t* cumul = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(rk) + SIZE + 1024);
@@ -906,8 +908,8 @@ __global__ __launch_bounds__(64) void dtable_blocks_kernel(DtParams P) {
         // two-pass ranks need 2^L / 64 per-chunk registers: up to L = 12
         const RankAtomic ra{P.peer_ranks == 0u, occ, nullptr, 0u, &g_rank_fb_dec, P.rank_inject};
         if (LMAX <= 12)
-            rc = wave_build_spread<SIZE / 64u, true>(norm, L, tl, sym_at, occ, cumul, cnt, visit, first_x, ra, rk, pm,
-                                               &P);
+            rc = wave_build_spread<SIZE / 64u, true>(norm, L, tl, sym_at, occ, cumul, cnt, visit, first_x, ra, rk,
+                                                     nullptr, &P);
         else rc = wave_build_spread<64, true>(norm, L, tl, sym_at, occ, cumul, cnt, visit, first_x, ra);
     }
     FSE_STAMP(P, 8);

@@ -23,6 +23,7 @@
 #                      rounds, C2 bytes checked against the first build's digest
 #   abdec:V1,V2,...    decode A/B (tools/time_dec.py: C3, C2 encode / decode, exactness),
 #                      three alternating rounds
+#   abpy:SCRIPT:V1,... any tools/SCRIPT.py timing script, three alternating rounds over the builds
 #
 # Variant libraries (FSEHIP_LIB=libfsehip_NAME.so) are selected by the caller's
 # environment: FSEHIP_LIB=libfsehip_diag.so tools/gpu_run.sh OUT bench ...
@@ -97,6 +98,15 @@ for step in "$@"; do
         done
       done
       grep '^{' "$O/abdec.txt" ;;
+    abpy)
+      script=${arg%%:*}; vs=${arg#*:}
+      for r in 1 2 3; do
+        for v in ${vs//,/ }; do
+          lib=libfsehip_$v.so; [ "$v" = product ] && lib=libfsehip.so
+          FSEHIP_LIB=$lib timeout -k 10 300 python3 "tools/$script.py" >> "$O/$script.txt" 2>&1 || fail "$step" $? "$O/$script.txt"
+        done
+      done
+      grep -v amdgpu.ids "$O/$script.txt" ;;
     *)
       echo "unknown step '$step'"; exit 2 ;;
   esac
