@@ -2087,7 +2087,10 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
     // PB12: the L = 12 list pass's stage, the most that keeps 2 workgroups per
     // CU beside its 16 KiB table (near-uniform blocks at L = 12, ~65.3 KB,
     // fit; 1 per CU with a 66 KiB stage)
-    constexpr uint32_t PP = 44u << 10, PB = 66u << 10, PB12 = 65392u;
+#ifndef FSE_DEC_PP
+#define FSE_DEC_PP (44u << 10)  // a variant build may lower it (occupancy probes)
+#endif
+    constexpr uint32_t PP = FSE_DEC_PP, PB = 66u << 10, PB12 = 65392u;
     static const uint32_t cus = [] {
         int dev = 0, n = 0;
         (void)hipGetDevice(&dev);

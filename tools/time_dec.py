@@ -29,7 +29,7 @@ blocks = int(os.environ.get("C3_BLOCKS", 32768))
 ckpt = int(os.environ.get("CKPT", 64))
 codec = BlockCodec(block_size=65536, ckpt_interval=ckpt)
 n = blocks * 65536
-src = codec.generate(0, 0.155, 0x5EED0003, n)
+src = codec.generate(0, float(os.environ.get("P", 0.155)), 0x5EED0003, n)  # P: the LUT skew (probes)
 cb = codec.compress(src)
 tabs = codec.build_dtables(cb)
 out = torch.empty_like(src)
@@ -53,5 +53,5 @@ ok2 = ok2 and bytes_ok
 comp3 = int(cb["comp_len"].to(torch.int64).sum())
 side = blocks * codec.side_per_block * 8
 frac = (comp3 + side + n) / (c3 * 1e-3) / 8e12
-print(json.dumps({"lib": os.environ.get("FSEHIP_LIB", "libfsehip.so"), "ckpt": ckpt, "c3_ms": round(c3, 4), "c3_frac": round(frac, 3),
+print(json.dumps({"lib": os.environ.get("FSEHIP_LIB", "libfsehip.so"), "p": float(os.environ.get("P", 0.155)), "ckpt": ckpt, "c3_ms": round(c3, 4), "c3_frac": round(frac, 3),
                   "c3_exact": ok3, "c2_encode_ms": round(enc, 4), "c2_decode_ms": round(dec, 4), "c2_exact": ok2}))
