@@ -1183,6 +1183,16 @@ __global__ __launch_bounds__(64) void serial2_decode_kernel(DecParams P) {
 // Same end checks, statuses and sidecar recording as serial2.
 // ------------------------------------------------------------------------
 constexpr uint32_t RING_WORDS = 128u, RING_MASK = RING_WORDS - 1u, RING_CHUNK = 64u;
+#ifndef FSE_RING_GROUP
+#define FSE_RING_GROUP 32
+#endif
+// state words (pairs, or two 1-state symbols) per bulk iteration with the
+// symbols deferred; a multiple of 8 (whole 16-byte groups for sym_map_kernel).
+// The loop's control (~45 instructions an iteration: the ring wait, the
+// stores, the published position) is paid once per group: C2 sidecar-less
+// decode 8.07 ms at 8, 7.31 at 16, 7.01 at 32, 7.20 at 64 (profiles/r06/rg/)
+constexpr uint32_t RING_GROUP = FSE_RING_GROUP;
+static_assert(RING_GROUP % 8u == 0u && RING_GROUP <= 64u, "ring group: the tail waits for (2 RING_GROUP + 4) L bits, 45 words at 64");
 
 // Relaxed workgroup-scope atomics keep these as plain ds_read/ds_write (a
 // volatile access through a generic pointer becomes a FLAT access that
@@ -1281,7 +1291,12 @@ struct RingChain {
     // the 32 bits [pos - 32, pos); below bit 0 (pos < 32) the low bits are
     // stale ring contents that no step uses
     __device__ __forceinline__ uint32_t window() const {
-        const uint32_t a = R + (__builtin_amdgcn_ubfe((uint32_t)p32, 5u, 7u) << 2);
+        // one v_bfe and one v_lshl_add (from ubfe << 2 the compiler makes a
+        // shift, a mask and an add: one VALU more per pair, 1.7 % of the
+        // sidecar-less decode, profiles/r06/rg/)
+        uint32_t wi;
+        asm("v_bfe_u32 %0, %1, 5, 7" : "=v"(wi) : "v"(p32));
+        const uint32_t a = R + (wi << 2);
         return __builtin_amdgcn_alignbit(lds_u32_at(a + 4u), lds_u32_at(a), (uint32_t)p32);
     }
     // one pair; returns sym0 | sym1 << 8
@@ -1519,20 +1534,23 @@ __global__ __launch_bounds__(64 * (DW + 1)) void serial_ring_kernel(DecParams P)
                 next_ck = ck < P.ckpt_per_block ? next_ck + I : 0xFFFFFFFFu;
             }
         };
-        // bulk: 16 output bytes (8 pairs / 16 symbols, <= 16L bits) without end
-        // checks; the checkpoint compare is compiled in only when recording
+        // bulk: 2GS output bytes (GS pairs / 2GS symbols, <= 2GS L bits) without
+        // end checks; the checkpoint compare is compiled in only when recording.
+        // GS = 8, or RING_GROUP with the symbols deferred (fewer loop-control
+        // instructions per pair)
+        constexpr uint32_t GS = DEF ? RING_GROUP : 8u;
         auto bulk = [&](auto rec_on) {
             constexpr bool REC = decltype(rec_on)::value;
             auto record = [&]() {
                 if (REC) record_at(c.pos(), c.s0(T), c.s1(T));
             };
-            while (o + 18u < lim && c.pos() - hdr_bits >= 16 * (int32_t)L) {
-                wait_words((c.pos() - 32 - 16 * (int32_t)L) >> 5);
+            while (o + 2u * GS + 2u < lim && c.pos() - hdr_bits >= 2 * (int32_t)GS * (int32_t)L) {
+                wait_words((c.pos() - 32 - 2 * (int32_t)GS * (int32_t)L) >> 5);
                 uint32_t w[4];
-                if constexpr (DEF) {  // the states of 16 symbols, 32 bytes per 16 output bytes
-                    uint32_t v[8];
+                if constexpr (DEF) {  // the states of 2GS symbols, 2 bytes per output byte
+                    uint32_t v[GS];
 #pragma unroll
-                    for (uint32_t j = 0; j < 8u; ++j) {
+                    for (uint32_t j = 0; j < GS; ++j) {
                         if constexpr (NS == 2) {
                             v[j] = c.pair_states(T);
                         } else {
@@ -1541,9 +1559,10 @@ __global__ __launch_bounds__(64 * (DW + 1)) void serial_ring_kernel(DecParams P)
                         }
                     }
                     uint4* sp = reinterpret_cast<uint4*>(st_out + (o >> 1));
-                    sp[0] = make_uint4(v[0], v[1], v[2], v[3]);
-                    sp[1] = make_uint4(v[4], v[5], v[6], v[7]);
-                    o += 16;
+#pragma unroll
+                    for (uint32_t q = 0; q < GS / 4u; ++q)
+                        sp[q] = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+                    o += 2u * GS;
                     lds_store_volatile(&ctl[1], c.pos() >> 5);
                     continue;
                 } else if constexpr (NS == 2) {
@@ -1579,12 +1598,12 @@ __global__ __launch_bounds__(64 * (DW + 1)) void serial_ring_kernel(DecParams P)
         else if (rec) bulk(std::true_type{});
         else bulk(std::false_type{});
         o_bulk = o;
-        // the tail reads words <= pos/32 + 1, and it ends within 16L bits
-        // (bulk stopped by the position) or within 18 steps (stopped by the
-        // output limit): wait for just those words, the loader cannot pass
+        // the tail reads words <= pos/32 + 1, and it ends within 2GS L bits
+        // (bulk stopped by the position) or within 2GS + 2 symbols (stopped by
+        // the output limit): wait for just those words, the loader cannot pass
         // the ring's words above what the decoder still reads
         lds_store_volatile(&ctl[1], (c.pos() >> 5) + 1);
-        wait_words(max(hdr_bits, c.pos() - 20 * (int32_t)L) >> 5);
+        wait_words(max(hdr_bits, c.pos() - (2 * (int32_t)GS + 4) * (int32_t)L) >> 5);
         uint32_t s0 = c.s0(T), s1 = c.s1(T);
         int32_t pos = c.pos();
         auto pop = [&](uint32_t nb) -> uint32_t {
