@@ -1192,6 +1192,15 @@ constexpr uint32_t RING_WORDS = 128u, RING_MASK = RING_WORDS - 1u, RING_CHUNK = 
 // stores, the published position) is paid once per group: C2 sidecar-less
 // decode 8.07 ms at 8, 7.31 at 16, 7.01 at 32, 7.20 at 64 (profiles/r06/rg/)
 constexpr uint32_t RING_GROUP = FSE_RING_GROUP;
+#ifndef FSE_RING_GROUP_SYM
+#define FSE_RING_GROUP_SYM 32
+#endif
+// the same for the kernels that write the symbols themselves (L = 12, the
+// fallback without the state workspace, sidecar rebuilds): 32 against 8,
+// skewed L = 12 sidecar-less 17.5 -> 16.3 ms per GiB, C2 sidecar rebuild
+// 11.7 -> 10.7 ms (profiles/r06/rg/)
+constexpr uint32_t RING_GROUP_SYM = FSE_RING_GROUP_SYM;
+static_assert(RING_GROUP_SYM % 8u == 0u && RING_GROUP_SYM <= 64u, "ring group");
 static_assert(RING_GROUP % 8u == 0u && RING_GROUP <= 64u, "ring group: the tail waits for (2 RING_GROUP + 4) L bits, 45 words at 64");
 
 // Relaxed workgroup-scope atomics keep these as plain ds_read/ds_write (a
@@ -1538,7 +1547,7 @@ __global__ __launch_bounds__(64 * (DW + 1)) void serial_ring_kernel(DecParams P)
         // end checks; the checkpoint compare is compiled in only when recording.
         // GS = 8, or RING_GROUP with the symbols deferred (fewer loop-control
         // instructions per pair)
-        constexpr uint32_t GS = DEF ? RING_GROUP : 8u;
+        constexpr uint32_t GS = DEF ? RING_GROUP : RING_GROUP_SYM;
         auto bulk = [&](auto rec_on) {
             constexpr bool REC = decltype(rec_on)::value;
             auto record = [&]() {
@@ -1546,9 +1555,10 @@ __global__ __launch_bounds__(64 * (DW + 1)) void serial_ring_kernel(DecParams P)
             };
             while (o + 2u * GS + 2u < lim && c.pos() - hdr_bits >= 2 * (int32_t)GS * (int32_t)L) {
                 wait_words((c.pos() - 32 - 2 * (int32_t)GS * (int32_t)L) >> 5);
-                uint32_t w[4];
-                if constexpr (DEF) {  // the states of 2GS symbols, 2 bytes per output byte
-                    uint32_t v[GS];
+                // DEF: the states of 2GS symbols, 2 bytes per output byte; else
+                // the 2GS symbols themselves
+                uint32_t v[DEF ? GS : GS / 2u];
+                if constexpr (DEF) {
 #pragma unroll
                     for (uint32_t j = 0; j < GS; ++j) {
                         if constexpr (NS == 2) {
@@ -1558,27 +1568,20 @@ __global__ __launch_bounds__(64 * (DW + 1)) void serial_ring_kernel(DecParams P)
                             v[j] = __builtin_amdgcn_perm(c.step_state(T), a, 0x05040100u);
                         }
                     }
-                    uint4* sp = reinterpret_cast<uint4*>(st_out + (o >> 1));
-#pragma unroll
-                    for (uint32_t q = 0; q < GS / 4u; ++q)
-                        sp[q] = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
-                    o += 2u * GS;
-                    lds_store_volatile(&ctl[1], c.pos() >> 5);
-                    continue;
                 } else if constexpr (NS == 2) {
 #pragma unroll
-                    for (uint32_t j = 0; j < 8u; j += 2u) {
+                    for (uint32_t j = 0; j < GS; j += 2u) {
                         record();
                         const uint32_t lo = c.pair(T);
                         ++pidx;
                         record();
                         const uint32_t hi = c.pair(T);
                         ++pidx;
-                        w[j >> 1] = lo | (hi << 16);
+                        v[j >> 1] = lo | (hi << 16);
                     }
                 } else {
 #pragma unroll
-                    for (uint32_t j = 0; j < 4u; ++j) {
+                    for (uint32_t j = 0; j < GS / 2u; ++j) {
                         uint32_t y = 0;
 #pragma unroll
                         for (uint32_t q = 0; q < 4u; ++q) {
@@ -1586,11 +1589,14 @@ __global__ __launch_bounds__(64 * (DW + 1)) void serial_ring_kernel(DecParams P)
                             y |= c.step(T) << (8u * q);
                             ++pidx;
                         }
-                        w[j] = y;
+                        v[j] = y;
                     }
                 }
-                *reinterpret_cast<uint4*>(out + o) = make_uint4(w[0], w[1], w[2], w[3]);
-                o += 16;
+                uint4* sp = DEF ? reinterpret_cast<uint4*>(st_out + (o >> 1)) : reinterpret_cast<uint4*>(out + o);
+#pragma unroll
+                for (uint32_t q = 0; q < (DEF ? GS : GS / 2u) / 4u; ++q)
+                    sp[q] = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+                o += 2u * GS;
                 lds_store_volatile(&ctl[1], c.pos() >> 5);  // the highest word a later step reads
             }
         };
