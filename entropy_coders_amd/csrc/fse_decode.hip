@@ -1545,8 +1545,8 @@ __global__ __launch_bounds__(64 * (DW + 1)) void serial_ring_kernel(DecParams P)
         };
         // bulk: 2GS output bytes (GS pairs / 2GS symbols, <= 2GS L bits) without
         // end checks; the checkpoint compare is compiled in only when recording.
-        // GS = 8, or RING_GROUP with the symbols deferred (fewer loop-control
-        // instructions per pair)
+        // GS = RING_GROUP with the symbols deferred, RING_GROUP_SYM otherwise
+        // (both 32: the loop's control is paid once per 32 pairs)
         constexpr uint32_t GS = DEF ? RING_GROUP : RING_GROUP_SYM;
         auto bulk = [&](auto rec_on) {
             constexpr bool REC = decltype(rec_on)::value;
