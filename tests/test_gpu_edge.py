@@ -209,6 +209,59 @@ def test_sidecar_less_partial_groups(torch_cuda, table_log, n_blocks):
     assert torch.equal(side2, cb["sidecar"])
 
 
+@pytest.mark.parametrize("nstates", [2, 1])
+def test_sidecar_less_bulk_tail_boundary(torch_cuda, nstates):
+    """The sidecar-less decoder's bulk loop runs 32 state words (64 symbols)
+    between end checks and leaves the rest to the checked tail: lengths and
+    capacities on either side of that boundary, in container mode (raw
+    length known, ragged last blocks) and in the crate's own termination
+    (fsehip_decompress_streams at several strides), against the oracle."""
+    torch = torch_cuda
+    from entropy_coders_amd import BlockCodec, decompress_streams
+
+    rng = np.random.default_rng(0xB0B0 + nstates)
+    for block in (64, 80, 128, 144, 192, 4096 + 64):  # multiples of 16 (several blocks)
+        sizes = [block] * 5 + [int(rng.integers(2, block + 1))]
+        host = np.concatenate([O.generate(0, float(rng.uniform(0.05, 0.6)), int(rng.integers(1 << 30)), 0, m)
+                               for m in sizes])
+        codec = BlockCodec(block_size=block, ckpt_interval=0, nstates=nstates)
+        src = torch.from_numpy(host).cuda()
+        cb = codec.compress(src)
+        out, st = codec.decompress(cb, use_sidecar=False)
+        torch.cuda.synchronize()
+        for b, m in enumerate(sizes):
+            lo = b * block
+            seg = host[lo: lo + m]
+            try:
+                (O.compress2 if nstates == 2 else O.compress)(seg)
+            except O.OracleError:
+                assert int(st[b]) != 0, (block, b)
+                continue
+            assert int(st[b]) == 0, (block, b, int(st[b]))
+            assert np.array_equal(out[lo: lo + m].cpu().numpy(), seg), (block, b)
+    comp = (lambda x: O.compress2(x, None)[0]) if nstates == 2 else (lambda x: O.compress(x)[0])
+    dec = O.decompress2 if nstates == 2 else O.decompress
+    lens = list(range(3, 80)) + list(range(124, 140)) + [4096 + 60, 4096 + 66, 4096 + 70]
+    streams = []
+    for m in lens:
+        x = O.generate(0, float(rng.uniform(0.05, 0.6)), int(rng.integers(1 << 30)), 0, m)
+        if len(set(x.tolist())) < 2:
+            continue
+        try:
+            streams.append(comp(x))
+        except O.OracleError:
+            continue
+    for stride in (64, 80, 128, 144, 4096 + 64, 8192):  # multiples of 16 (the ABI)
+        got = decompress_streams(streams, stride, nstates=nstates, max_table_log=11)
+        for i, (x, g) in enumerate(zip(streams, got)):
+            try:
+                want = dec(x, stride)
+            except O.OracleError as e:
+                assert g == e.code, (stride, i, e.code, g)
+                continue
+            assert g == want, (stride, i)
+
+
 @pytest.mark.parametrize("seed", range(6))
 @pytest.mark.parametrize("nstates", [2, 1])
 def test_random_corruption_never_hangs(torch_cuda, seed, nstates):
