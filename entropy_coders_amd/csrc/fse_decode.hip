@@ -2181,6 +2181,9 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
         } else if (lmax <= 14) {
             run(decode_pre_kernel<14, PP, 2, 1>, 1, 0);
             run(decode_pre_kernel<14, PB, 2, 2>, 2, 1);
+        } else if (wide) {  // 128 KiB table: 1 workgroup per CU, 8 waves instead of 4
+            // (near-uniform C5 L = 15 decode 72.7 -> 77.2 GiB/s, profiles/r06/w15/)
+            run(decode_pre_kernel<15, 16, 2, 0, 512>, 0, 0, 512);
         } else {
             run(decode_pre_kernel<15, 16, 2, 0>, 0, 0);
         }
