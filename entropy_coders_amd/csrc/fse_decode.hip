@@ -384,45 +384,57 @@ __device__ __forceinline__ int32_t run_chain(Chain& c, const uint32_t* pay, cons
                        });
 }
 
-// 1-state chain (fse_decompress blocks): one state, one symbol per step,
-// a per-lane 64-bit window over words (k, k+1) refilled a word at a time
-// with the next word prefetched a refill ahead.
+// 1-state chain (fse_decompress blocks) without a refill branch (round 6;
+// the register window it replaced refilled under a divergent branch every
+// few symbols and needed 110 VGPRs, 2 workgroups per CU at 512 threads:
+// C2 1-state decode 0.75-0.78 -> 0.57 ms per GiB, profiles/r06/w1/): each call
+// cuts x = the 32 bits just below pos from the word pair around pos - 32
+// (word pos / 32 carried from the previous call, the word below it read:
+// one ds_read, a compare, a select and a v_alignbit), then takes one symbol's
+// field (step) or two symbols' fields (pair: <= 2 x 14 bits) from the top
+// of x.  The image has 16 pad bytes below it (the word below word 0).
 struct LdsChain1 {
-    int32_t pos, B;
-    uint32_t wlo, whi, wnx, a;
+    int32_t pos;
+    uint32_t Q, whi, wlo, a;
     __device__ __forceinline__ void init(const uint32_t* pay, int32_t p, uint32_t s) {
         pos = p;
         a = s << 2;
-        const int32_t k = max((p >> 5) - 1, 0);
-        B = k << 5;
-        wlo = pay[k];
-        whi = pay[k + 1];
-        wnx = pay[max(k - 1, 0)];
+        Q = ((uint32_t)p >> 3) & ~3u;
+        wlo = 0;
+        whi = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(pay) + Q);
+    }
+    __device__ __forceinline__ uint32_t window(const uint32_t* pay) {
+        const uint32_t q = ((uint32_t)pos >> 3) & ~3u;
+        const uint32_t wq = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(pay) + q - 4u);
+        const uint32_t hi = q == Q ? whi : wlo;
+        Q = q;
+        whi = hi;
+        wlo = wq;
+        return __builtin_amdgcn_alignbit(hi, wq, (uint32_t)pos);
     }
     // one symbol; returns the table entry (symbol in bits 8-15)
     __device__ __forceinline__ uint32_t step(const uint32_t* pay, const uint8_t* dtb) {
         const uint32_t e = *reinterpret_cast<const uint32_t*>(dtb + a);
+        const uint32_t x = window(pay);
         pos -= (int32_t)(e & 0xFFu);
-        const uint32_t x = (uint32_t)((((uint64_t)whi << 32) | wlo) >> (uint32_t)(pos - B));
-        if (pos < B + 32) {
-            B -= 32;
-            whi = wlo;
-            wlo = wnx;
-            wnx = pay[max((B >> 5) - 1, 0)];
-        }
-        a = (e >> 16) + (__builtin_amdgcn_ubfe(x, 0u, e) << 2);
+        a = (e >> 16) + (__builtin_amdgcn_ubfe(x, 0u - e, e) << 2);
         return e;
     }
-};
-
-// A 1-state chain as two steps per call (sym0 | sym1 << 8), for the
-// transposed group stores (run_groups_tx)
-struct Chain1x2 {
-    LdsChain1 c;
+    // two symbols from one window; returns sym0 | sym1 << 8
     __device__ __forceinline__ uint32_t pair(const uint32_t* pay, const uint8_t* dtb) {
-        const uint32_t e0 = c.step(pay, dtb), e1 = c.step(pay, dtb);
+        const uint32_t e0 = *reinterpret_cast<const uint32_t*>(dtb + a);
+        const uint32_t x = window(pay);
+        const uint32_t o0 = 0u - e0;  // low 5 bits: 32 - nb0
+        const uint32_t a1 = (e0 >> 16) + (__builtin_amdgcn_ubfe(x, o0, e0) << 2);
+        const uint32_t e1 = *reinterpret_cast<const uint32_t*>(dtb + a1);
+        a = (e1 >> 16) + (__builtin_amdgcn_ubfe(x, o0 - e1, e1) << 2);
+        pos -= (int32_t)((e0 + e1) & 0xFFu);
         return __builtin_amdgcn_perm(e1, e0, 0x0c0c0501u);
     }
+};
+struct Chain1x2 {
+    LdsChain1 c;
+    __device__ __forceinline__ uint32_t pair(const uint32_t* pay, const uint8_t* dtb) { return c.pair(pay, dtb); }
 };
 
 // Steps [p, p1) of one 1-state segment; the last segment then emits the
@@ -436,10 +448,8 @@ __device__ __forceinline__ int32_t run_chain1(LdsChain1& c, const uint32_t* pay,
         uint32_t w[G / 4u];
 #pragma unroll
         for (uint32_t j = 0; j < G; j += 4u) {
-            const uint32_t e0 = c.step(pay, dtb), e1 = c.step(pay, dtb);
-            const uint32_t e2 = c.step(pay, dtb), e3 = c.step(pay, dtb);
-            w[j >> 2] = __builtin_amdgcn_perm(__builtin_amdgcn_perm(e3, e2, 0x0c0c0501u),
-                                              __builtin_amdgcn_perm(e1, e0, 0x0c0c0501u), 0x05040100u);
+            const uint32_t lo = c.pair(pay, dtb), hi = c.pair(pay, dtb);
+            w[j >> 2] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
         }
         uint4* o4 = reinterpret_cast<uint4*>(out + p);
 #pragma unroll

@@ -100,6 +100,7 @@ GUARDS = [
     ("_ZN6fsehip20encode_blocks_kernelILi11ELi64ELi1EE", 14768, 11),   # 1-state encode
     ("_ZN6fsehip17decode_pre_kernelILi11ELj45056ELi2ELi1ELj512EE", 53296, 3),  # C2/C3 segment decode
     ("_ZN6fsehip17decode_pre_kernelILi11ELj45056ELi2ELi1ELj256EE", 53280, 3),  # 128-pair checkpoints
+    ("_ZN6fsehip17decode_pre_kernelILi11ELj45056ELi1ELi1ELj512EE", 53296, 3),  # 1-state segment decode
     ("_ZN6fsehip20dtable_blocks_kernelILi11EE", 7168, 22),             # decode tables
     ("_ZN6fsehip18serial_ring_kernelILi11ELj8ELi2ELb1ELj1EE", 37088, 4),  # sidecar-less decode
     ("_ZN6fsehip17decode_pre_kernelILi11ELj67584ELi2ELi2ELj512EE", 75888, 2),  # list pass (near-uniform blocks)
