@@ -43,7 +43,8 @@ enum {
     SCRATCH_STATES = 3,
     SCRATCH_BULK = 4,
     SCRATCH_HDR = 5,  // the lane-parallel header parse's output (optional)
-    SCRATCH_KINDS = 6
+    SCRATCH_SPREAD = 6,  // the L >= 13 encoder's spread symbols when the slots cannot hold them
+    SCRATCH_KINDS = 7
 };
 struct Workspace {
     int dev;
@@ -444,6 +445,15 @@ int fsehip_compress_blocks(const fsehip_params* p, const uint8_t* d_src, uint64_
     P.rank_inject = env_u32("FSEHIP_RANK_INJECT", 0);  // diagnostics: fault injection into the atomic ranks
     const size_t groups = (n_blocks * P.lanes + 63) / 64;
     P.stamps = g_stamps_enc.get(groups);
+    // the L >= 13 kernels keep the spread's 2^lmax symbols in global memory:
+    // in each block's slot after its header words when the slot has room,
+    // else in a workspace buffer (held until the launch is enqueued)
+    std::unique_ptr<Lease> lease;
+    if (fsehip::enc_gsym(lmax) && slot_bytes < fsehip::ENC_SPREAD_OFF + (1ull << lmax)) {
+        lease = std::make_unique<Lease>(stream);
+        P.spread = static_cast<uint8_t*>(lease->get(SCRATCH_SPREAD, n_blocks << lmax));
+        if (!P.spread) return FSE_ERR_HIP;
+    }
     hipError_t e = fsehip::launch_encode(P, lmax, static_cast<hipStream_t>(stream));
     if (P.stamps) g_stamps_enc.report("encode", groups, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? FSE_OK : FSE_ERR_HIP;

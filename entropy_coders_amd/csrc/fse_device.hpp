@@ -769,9 +769,25 @@ struct RankAtomic {
     uint32_t inject;      // diagnostics build only: chunk 0's ranks in descending lane order (fault injection)
 };
 
+// Is slot x the first slot of some symbol (x == cumul[s] for an s with
+// slots)?  cumul is non-decreasing over all 256 symbols (a symbol without
+// slots repeats the next start), so a lower-bound search answers it.
+__device__ __forceinline__ bool is_start_slot(const uint16_t* cumul, uint32_t x) {
+    uint32_t lo = 0;
+#pragma unroll
+    for (uint32_t h = 128; h; h >>= 1)
+        if ((uint32_t)cumul[lo + h - 1u] < x) lo += h;
+    return lo < 256u && (uint32_t)cumul[lo] == x;
+}
+
 // MAXCH: 2^LMAX / 64 chunks (two-pass ranks); INV: the atomic ranks' check in
-// inverse mode (RankAtomic::inv8), else in stateTable mode (RankAtomic::st)
-template <uint32_t MAXCH = 64, bool INV = false, typename Visit, typename Base, class SP = NoStamps>
+// inverse mode (RankAtomic::inv8), else in stateTable mode (RankAtomic::st);
+// GSYM: sym_at is in global memory (the encoder at L >= 13, whose LDS then
+// holds two or more workgroups per CU): its writes are fenced before other
+// lanes read them, the rank pass keeps several chunks' loads in flight, and
+// the stateTable check tests slot starts in cumul instead of reading symbols
+template <uint32_t MAXCH = 64, bool INV = false, bool GSYM = false, typename Visit, typename Base,
+          class SP = NoStamps>
 __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_t tl, uint8_t* sym_at,
                                         uint8_t* occ_sym, uint16_t* cumul, uint32_t* cnt, Visit visit, Base base,
                                         const RankAtomic& ra, uint16_t* RK = nullptr, uint64_t* PM = nullptr,
@@ -810,6 +826,7 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
         reinterpret_cast<uint4*>(occ_sym)[i] = make_uint4(0, 0, 0, 0);
         reinterpret_cast<uint4*>(sym_at)[i] = make_uint4(0, 0, 0, 0);
     }
+    if (GSYM) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     wave_sync();
     {
         uint32_t c = ex_c, p = ex_p, ng = ex_n;
@@ -824,6 +841,7 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
             ng += neg[k];
         }
     }
+    if (GSYM) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     wave_sync();
     // forward max-fill: occ_sym[j] = owner of positive occurrence j (4 per
     // lane; entries at and above total_pos are filled too and never read)
@@ -876,6 +894,7 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
         }
         if (j0 != total_pos) return FSE_ERR_BAD_TABLE;  // position != 0 assert
     }
+    if (GSYM) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     wave_sync();
     SPREAD_STAMP(5);
     if (ra.on) {
@@ -901,12 +920,23 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
         // the next chunk's symbols are read while this chunk's atomics are in
         // flight; in inverse mode the counter is read back right behind the
         // atomic (a wave's LDS instructions run in order), one wait for both
-        uint32_t sy_next = lane < size ? sym_at[lane] : 0u;
+        // (GSYM: GD chunks' symbols in flight, a global load's latency being
+        // several iterations long)
+        constexpr uint32_t GD = GSYM ? 8u : 1u;
+        uint32_t sy_q[GD];
+#pragma unroll
+        for (uint32_t k = 0; k < GD; ++k) sy_q[k] = k * WAVE + lane < size ? sym_at[k * WAVE + lane] : 0u;
         for (uint32_t i0 = 0; i0 < size; i0 += WAVE) {
             const uint32_t i = i0 + lane;
             const bool act = i < size;
-            const uint32_t sy = sy_next;
-            if (i + WAVE < size) sy_next = sym_at[i + WAVE];
+            const uint32_t sy = sy_q[0];
+            if constexpr (GSYM) {
+#pragma unroll
+                for (uint32_t k = 0; k + 1u < GD; ++k) sy_q[k] = sy_q[k + 1u];
+                sy_q[GD - 1u] = i + GD * WAVE < size ? sym_at[i + GD * WAVE] : 0u;
+            } else {
+                if (i + WAVE < size) sy_q[0] = sym_at[i + WAVE];
+            }
             uint32_t r = 0, endw = 0;
             if (act) {
                 r = __hip_atomic_fetch_add((lds_u32*)cnt + sy, step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -959,8 +989,13 @@ __device__ inline int wave_build_spread(const int32_t* norm, uint32_t L, uint32_
                     const uint32_t v[5] = {w.x & 0xFFFFu, w.x >> 16, w.y & 0xFFFFu, w.y >> 16,
                                            g + 4u < size ? (uint32_t)ra.st[g + 4u] : 0xFFFFFu};
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        if (v[j] > v[j + 1] && sym_at[v[j] - ra.st_off] == sym_at[v[j + 1] - ra.st_off]) bad = true;
+                    for (int j = 0; j < 4; ++j) {
+                        if (GSYM) {
+                            if (v[j] > v[j + 1] && !is_start_slot(cumul, g + (uint32_t)j + 1u)) bad = true;
+                        } else {
+                            if (v[j] > v[j + 1] && sym_at[v[j] - ra.st_off] == sym_at[v[j + 1] - ra.st_off]) bad = true;
+                        }
+                    }
                 }
             }
         }

@@ -30,7 +30,17 @@ struct EncParams {
     uint32_t xlds;            // diagnostics: extra dynamic LDS bytes per workgroup (occupancy probe)
     uint32_t peer_ranks;      // set by launch_encode: 1 = peer-mask ranks (forced by rank_mode)
     uint32_t rank_inject;     // diagnostics build only: fault injection into the atomic ranks (FSEHIP_RANK_INJECT)
+    // kernels at L >= 13 (enc_gsym): the spread's 2^LMAX-byte symbol array of
+    // block b at spread + b * 2^LMAX, or (nullptr) in the block's own output
+    // slot after its header words, when slot_bytes >= HDR_MAX + 2^LMAX
+    uint8_t* spread;
 };
+// Encoder kernels whose spread symbol array lives in global memory (L >= 13):
+// their LDS then fits 7 / 4 / 2 workgroups per CU at L = 13 / 14 / 15
+// instead of 5 / 3 / 1.
+constexpr bool enc_gsym(uint32_t lmax) { return lmax >= 13u; }
+// byte offset of the in-slot spread array (after the header words, <= 512 B)
+constexpr uint32_t ENC_SPREAD_OFF = 512;
 
 struct DecParams {
     const uint8_t* in;

@@ -229,6 +229,9 @@ constexpr bool counts() { return MODE == PASS_COUNT || MODE == PASS_REPAIR; }
 // Trajectory slots per lane.  16 (repairs stop sooner) measured slower
 // than 8 on C2: the count pass writes twice as many slots.
 constexpr uint32_t TRACK_SLOTS = 8;
+// L >= 14: 7, so that the L = 14 kernel's LDS fits 4 workgroups per CU
+template <int LMAX>
+constexpr uint32_t track_slots() { return LMAX >= 14 ? TRACK_SLOTS - 1u : TRACK_SLOTS; }
 struct Track {
     uint32_t* cx;     // this lane's slots: state pairs (LDS)
     uint2* cb;        // this lane's slots: per-chain bit counts (LDS)
@@ -562,10 +565,26 @@ __device__ __forceinline__ EncState top_start(const uint8_t* blk, uint32_t n, co
 // ------------------------------------------------------------------------
 // Encode kernel
 // ------------------------------------------------------------------------
+// A block's phase-1 results read by phase 2, and phase 1's small scratch.
+template <int BPW>
+struct EncTail {
+    int32_t status[BPW];
+    uint32_t L[BPW];
+    uint32_t hl[BPW];
+    uint32_t hv[BPW];  // the header's last partial word (merged with the payload's first bits)
+    int scratch[4];
+};
+
 template <int LMAX, int T>
 struct EncSmem {
     static constexpr int BPW = 64 / T;
     static constexpr uint32_t SIZE = 1u << LMAX;
+    // L >= 14 (one block per wave): the tail lives in phase 2's trajectory
+    // struct, beside its 7 slots and under the ring: 32 bytes that take the
+    // L = 14 kernel to 40,960 B and 4 workgroups per CU.  Phase 2 reads it
+    // into registers before the emit ring overwrites it.
+    static constexpr bool TAIL_IN_P2 = LMAX >= 14;
+    static_assert(!TAIL_IN_P2 || BPW == 1, "one block per wave");
     // A block's stateTable and symbol transforms are built last in phase 1,
     // so until then they hold its scratch: the sub-histograms (16 copies,
     // 8 KiB, over st and tt when one block has the wave; 8 copies, 4 KiB,
@@ -586,7 +605,8 @@ struct EncSmem {
         struct {
             union {
                 uint32_t hdrw[HDR_MAX / 4];  // NCount header, stored to the slot before the spread
-                __attribute__((aligned(16))) uint8_t sym_at[SIZE];
+                // (L >= 13: the spread's symbols are in global memory, EncParams::spread)
+                __attribute__((aligned(16))) uint8_t sym_at[enc_gsym(LMAX) ? 16u : SIZE];
             } u;
             int32_t norm[256];
             uint16_t cumul[256];
@@ -597,9 +617,10 @@ struct EncSmem {
         // the boundary-word merge after it
         union {
             struct {
-                uint2 cb[64 * TRACK_SLOTS];     // trajectories (Track): per-chain bit counts
-                uint32_t cx[64 * TRACK_SLOTS];  // and state pairs
+                uint2 cb[64 * track_slots<LMAX>()];     // trajectories (Track): per-chain bit counts
+                uint32_t cx[64 * track_slots<LMAX>()];  // and state pairs
                 uint32_t cntF[BPW][T + 1];      // each lane's end state
+                EncTail<BPW> tail[TAIL_IN_P2 ? 1 : 0];
             } u;
             __attribute__((aligned(16))) uint32_t ring[64 * RING_STRIDE];  // emit: output ring per lane (Emit)
             struct {
@@ -608,17 +629,21 @@ struct EncSmem {
             } mg;
         } p2;
     } ph;
-    int32_t info_status[BPW];
-    uint32_t info_L[BPW];
-    uint32_t info_hl[BPW];
-    uint32_t info_hv[BPW];  // the header's last partial word (merged with the payload's first bits)
-    int scratch[4];
+    EncTail<BPW> tail_out[TAIL_IN_P2 ? 0 : 1];
+    __device__ __forceinline__ EncTail<BPW>& tail() {
+        if constexpr (TAIL_IN_P2) return ph.p2.u.tail[0];
+        else return tail_out[0];
+    }
 };
 
 template <int LMAX, int T, int NS>
 __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     constexpr int BPW = 64 / T;
     __shared__ EncSmem<LMAX, T> sm;
+    // the tail in phase 2's trajectory struct must sit above every phase-1 byte
+    static_assert(!EncSmem<LMAX, T>::TAIL_IN_P2 ||
+                      64u * track_slots<LMAX>() * 12u + 4u * (T + 1u) >= sizeof(sm.ph.p1),
+                  "tail overlaps phase-1 scratch");
 #define ENC_WGID ((uint64_t)blockIdx.x)
 #define ENC_SYNC() __syncthreads()
     const uint32_t lane = lane_id();
@@ -628,7 +653,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     for (int b = 0; b < BPW; ++b) {
         const uint64_t gb = ENC_WGID * BPW + b;
         if (gb >= P.n_blocks) {
-            if (lane == 0) sm.info_status[b] = 1;  // no block
+            if (lane == 0) sm.tail().status[b] = 1;  // no block
             continue;
         }
         const uint64_t off = gb * P.block_size;
@@ -647,13 +672,13 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
         uint32_t Lreq = P.table_log, L = 0, slow = 0;
         if (n == 0) rc = FSE_ERR_EMPTY;
         if (rc == FSE_OK && P.table_log == 0) rc = optimal_log2(n, tl, &Lreq);  // histogram.rs:301
-        if (rc == FSE_OK) rc = wave_normalize(counts, n, tl, Lreq, sm.ph.p1.norm, &L, &slow, sm.scratch);
+        if (rc == FSE_OK) rc = wave_normalize(counts, n, tl, Lreq, sm.ph.p1.norm, &L, &slow, sm.tail().scratch);
         if (rc == FSE_OK && n < 2) rc = FSE_ERR_TOO_SHORT;  // lib.rs:154/156 unwrap
         if (rc == FSE_OK && L > (uint32_t)LMAX) rc = FSE_ERR_UNSUPPORTED;
         FSE_STAMP(P, 2);
         if (rc == FSE_OK) {
             const int hl = wave_header_write(sm.ph.p1.norm, L, tl, sm.ph.p1.u.hdrw);
-            if (lane == 0) sm.scratch[1] = hl;
+            if (lane == 0) sm.tail().scratch[1] = hl;
             if (hl < 0) {
                 rc = hl;
             } else {
@@ -662,7 +687,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
                 const uint32_t* h = sm.ph.p1.u.hdrw;
                 uint32_t* gw = reinterpret_cast<uint32_t*>(P.out + gb * P.slot_bytes);
                 for (uint32_t w = lane; w < (uint32_t)hl / 4u; w += WAVE) gw[w] = h[w];
-                if (lane == 0) sm.info_hv[b] = (hl & 3) ? h[hl / 4] & ((1u << (8u * (hl & 3))) - 1u) : 0u;
+                if (lane == 0) sm.tail().hv[b] = (hl & 3) ? h[hl / 4] & ((1u << (8u * (hl & 3))) - 1u) : 0u;
             }
             wave_sync();  // the spread reuses the header's LDS
         }
@@ -671,7 +696,12 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
             const uint32_t size = 1u << L;
             uint16_t* st = sm.st[b];
             const uint16_t* cumul = sm.ph.p1.cumul;
-            rc = wave_build_spread(sm.ph.p1.norm, L, tl, sm.ph.p1.u.sym_at, reinterpret_cast<uint8_t*>(st), sm.ph.p1.cumul,
+            constexpr bool GSYM = enc_gsym(LMAX);
+            uint8_t* const sym_at = !GSYM ? sm.ph.p1.u.sym_at
+                                    : P.spread ? P.spread + gb * (uint64_t)(1u << LMAX)
+                                               : P.out + gb * P.slot_bytes + ENC_SPREAD_OFF;
+            static_assert(ENC_SPREAD_OFF >= HDR_MAX && ENC_SPREAD_OFF % 16u == 0u, "in-slot spread array");
+            rc = wave_build_spread<64, false, GSYM>(sm.ph.p1.norm, L, tl, sym_at, reinterpret_cast<uint8_t*>(st), sm.ph.p1.cumul,
                                    sm.ph.p1.cnt,
                                    [&](uint32_t i, uint32_t, uint32_t r) {
                                        st[r] = (uint16_t)(size + i);  // fse.rs:157-162 (r = cumul[s] + rank)
@@ -716,15 +746,16 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
                     return idx >= 0 && idx < (int32_t)size;
                 };
                 const bool ok = init_ok(blk[n - 1u]) && (NS == 1 || init_ok(blk[n - 2u]));
-                sm.scratch[2] = ok ? FSE_OK : FSE_ERR_ENCODER_INIT;
+                sm.tail().scratch[2] = ok ? FSE_OK : FSE_ERR_ENCODER_INIT;
             }
             wave_sync();
-            if (rc == FSE_OK) rc = sm.scratch[2];
+            if (rc == FSE_OK) rc = sm.tail().scratch[2];
         }
         if (lane == 0) {
-            sm.info_status[b] = rc;
-            sm.info_L[b] = L;
-            sm.info_hl[b] = (rc == FSE_OK) ? (uint32_t)sm.scratch[1] : 0u;
+            const uint32_t hl = (rc == FSE_OK) ? (uint32_t)sm.tail().scratch[1] : 0u;
+            sm.tail().status[b] = rc;
+            sm.tail().L[b] = L;
+            sm.tail().hl[b] = hl;
             if (rc != FSE_OK) {
                 P.status[gb] = rc;
                 P.comp_len[gb] = 0;
@@ -740,11 +771,15 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     const int b = BPW == 1 ? 0 : (int)(lane / T);
     const uint32_t k = BPW == 1 ? lane : lane % T;
     const uint64_t gb = ENC_WGID * BPW + b;
-    const bool live = sm.info_status[b] == FSE_OK;
+    const bool live = sm.tail().status[b] == FSE_OK;
+    // (TAIL_IN_P2: read now, the emit ring overwrites the tail)
+    using Sm2 = EncSmem<LMAX, T>;
+    const uint32_t hl_early = Sm2::TAIL_IN_P2 ? sm.tail().hl[b] : 0u;
+    const uint32_t hv_early = Sm2::TAIL_IN_P2 ? sm.tail().hv[b] : 0u;
     const uint64_t boff = gb * P.block_size;
     const uint32_t n = live ? (uint32_t)min((uint64_t)P.block_size, P.n_total - boff) : 0u;
     const uint8_t* blk = P.src + boff;
-    const uint32_t L = sm.info_L[b];
+    const uint32_t L = sm.tail().L[b];
     const EncTab tab{sm.tt[b]};
     // main-loop steps: pairs (NS = 2) or symbols below the seed (NS = 1)
     const uint32_t Pm = live ? (NS == 2 ? ((n & 1u) ? (n - 3u) / 2u : n / 2u - 1u) : n - 1u) : 0u;
@@ -764,8 +799,8 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     // start until the recorded trajectory is met) until the fixed point, then
     // the emit pass writes straight to the final offsets.  A repair round
     // costs the slowest lane's convergence distance.
-    Track tr{&sm.ph.p2.u.cx[lane * TRACK_SLOTS], &sm.ph.p2.u.cb[lane * TRACK_SLOTS],
-             max(1u, (S / SPC + TRACK_SLOTS - 1u) / TRACK_SLOTS), false, 0u};
+    constexpr uint32_t TS = track_slots<LMAX>();
+    Track tr{&sm.ph.p2.u.cx[lane * TS], &sm.ph.p2.u.cb[lane * TS], max(1u, (S / SPC + TS - 1u) / TS), false, 0u};
     const uint32_t nslot = pb > pa ? (((pb - 1u) / SPC) - (pa / SPC)) / tr.ckc + 1u : 0u;
     uint32_t start = (1u << L) | (NS == 2 ? (1u << L) << 16 : 0u);
     uint32_t bits = 0;
@@ -826,7 +861,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     if (kDiag && P.stamps && lane == 0)
         P.stamps[(uint64_t)blockIdx.x * kStamps + kStamps - 1] = (uint64_t)n_iter | ((uint64_t)n_rerun << 32);
     // offsets: lane k writes after every lane j > k (stack order)
-    const uint32_t hl = sm.info_hl[b];
+    const uint32_t hl = Sm2::TAIL_IN_P2 ? hl_early : sm.tail().hl[b];
     const uint32_t hdr_bits = hl * 8u;
     uint32_t mybits = act ? bits : 0u;
     uint32_t suffix = mybits;  // inclusive suffix sum over lanes >= k within the block
@@ -900,7 +935,7 @@ __global__ __launch_bounds__(64) void encode_blocks_kernel(EncParams P) {
     // header: whole words were stored in phase 1; the last partial word is merged
     if (live && fits && k == 0 && (hl & 3u)) {
         sm.ph.p2.mg.mword[b][0] = hl / 4u;
-        sm.ph.p2.mg.mval[b][0] = sm.info_hv[b];
+        sm.ph.p2.mg.mval[b][0] = Sm2::TAIL_IN_P2 ? hv_early : sm.tail().hv[b];
     }
     FSE_STAMP(P, 7);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stores above land before the merge rewrites
