@@ -323,7 +323,11 @@ uint32_t fsehip_sidecar_per_block_ns(uint32_t block_size, uint32_t ckpt_interval
  * Block b's bytes go to d_out + b*slot_bytes (comp_len[b] bytes, exactly
  * fse_compress2's output); d_sidecar (optional) receives the decode
  * checkpoints: entry = bitpos(32, payload-relative) | s0<<32 | s1<<48 for
- * the decoder state before pair k*ckpt_interval. */
+ * the decoder state before pair k*ckpt_interval.  A slot's bytes beyond
+ * comp_len[b] are unspecified: at table logs 13..15 the kernels use them
+ * as scratch (the spread's 2^L symbols after the first 512 bytes); slots
+ * smaller than 512 + 2^L bytes make the call take a workspace buffer of
+ * 2^L bytes per block instead (see fsehip_decompress_blocks). */
 int fsehip_compress_blocks(const fsehip_params* p, const uint8_t* d_src, uint64_t n_total, uint8_t* d_out,
                            uint64_t slot_bytes, uint32_t* d_comp_len, uint32_t* d_payload_bits,
                            uint64_t* d_sidecar, int32_t* d_status, fsehip_stream_t stream);
@@ -352,6 +356,9 @@ int fsehip_compress_blocks(const fsehip_params* p, const uint8_t* d_src, uint64_
  *                  1 GiB batch.  A size that failed to allocate is remembered
  *                  (later calls of that size or more take the single-kernel
  *                  decode without retrying) until the next release;
+ *   encode spread  2^L bytes per block (L the encode kernel's table log,
+ *                  13..15) when the slots are smaller than 512 + 2^L bytes
+ *                  (fsehip_compress_blocks);
  *   header parse   520 bytes per block (the headers parsed one per lane
  *                  before the table build: batches of >= 256 blocks at
  *                  max_table_log <= 12, fsehip_build_dtables included;
