@@ -512,7 +512,9 @@ __device__ __forceinline__ void decode_pre_block(const DecParams& P, Smem& sm, c
         if (tid == 0) P.status[gb] = info < 0 ? info : FSE_ERR_LENGTH_MISMATCH;
         return;
     }
-    if (P.pass == 1 && !in_lds) {  // too big for this stage: the list pass decodes it
+    // too big for this stage: a later list pass decodes it (pass 3: a list
+    // pass that defers its own oversized blocks again)
+    if ((P.pass == 1 || P.pass == 3) && !in_lds) {
         if (tid == 0) P.status[gb] = FSE_DEFERRED;
         return;
     }
@@ -2126,6 +2128,9 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
 #define FSE_DEC_PP (44u << 10)  // a variant build may lower it (occupancy probes)
 #endif
     constexpr uint32_t PP = FSE_DEC_PP, PB = 66u << 10, PB12 = 65392u;
+    // PS14: the small first stage at L = 14 (2 workgroups per CU beside the
+    // 64 KiB table)
+    constexpr uint32_t PS14 = 12u << 10;
     static const uint32_t cus = [] {
         int dev = 0, n = 0;
         (void)hipGetDevice(&dev);
@@ -2180,13 +2185,20 @@ hipError_t launch_decode(const DecParams& P, uint32_t lmax, hipStream_t stream) 
             run(decode_pre_kernel<12, PP - 8192, 2, 1>, 1, 0);
             run(decode_pre_kernel<12, PB12, 2, 2>, 2, 2);
         } else if (lmax <= 13 && wide) {  // 32 KiB table: 2 workgroups per CU, the list pass 1
+            // (a 16 KiB first stage, 3 per CU, measured a wash: skewed +2.5 %,
+            // near-uniform -1 %, profiles/r06/sd/)
             run(decode_pre_kernel<13, PP, 2, 1, 512>, 1, 0, 512);
             run(decode_pre_kernel<13, PB, 2, 2, 512>, 2, 1, 512);
         } else if (lmax <= 13) {
             run(decode_pre_kernel<13, PP, 2, 1>, 1, 0);
             run(decode_pre_kernel<13, PB, 2, 2>, 2, 1);
-        } else if (lmax <= 14 && wide) {  // 64 KiB table: 1 workgroup per CU
-            run(decode_pre_kernel<14, PP, 2, 1, 512>, 1, 0, 512);
+        } else if (lmax <= 14 && wide) {  // 64 KiB table
+            // a 12 KiB stage first (2 workgroups per CU: skewed blocks fit),
+            // then the 44 and 66 KiB stages as list passes (1 per CU): C5
+            // skewed L = 14 decode 342 -> 368 GiB/s, near-uniform unchanged
+            // (profiles/r06/sd/)
+            run(decode_pre_kernel<14, PS14, 2, 1, 512>, 1, 0, 512);
+            run(decode_pre_kernel<14, PP, 2, 3, 512>, 3, 1, 512);
             run(decode_pre_kernel<14, PB, 2, 2, 512>, 2, 1, 512);
         } else if (lmax <= 14) {
             run(decode_pre_kernel<14, PP, 2, 1>, 1, 0);
