@@ -847,9 +847,13 @@ __global__ __launch_bounds__(64) void dtable_blocks_kernel(DtParams P) {
     __shared__ __attribute__((aligned(16))) uint8_t sym_at[SIZE];
     // the two-pass rank table (2^L u16) reuses the occurrence owners, the
     // counters and cumul: all three are dead once the spread walk is done
-    // (the decoder's visit reads norm only); 7 KB per workgroup at L = 11
-    __shared__ __attribute__((aligned(16))) uint16_t rk[SIZE];
-    static_assert(SIZE + 256 * 4 + 256 * 2 <= SIZE * 2, "rank table must cover occ, cnt and cumul");
+    // (the decoder's visit reads norm only); 7 KB per workgroup at L = 11.
+    // L >= 13 never takes the two-pass ranks, so the array only has to hold
+    // occ, cnt and cumul: 2^L + 1.5 KiB instead of 2^(L+1) bytes (L = 15: 2
+    // workgroups per CU instead of 1)
+    constexpr uint32_t RKN = LMAX <= 12 ? SIZE : SIZE / 2u + 768u;
+    __shared__ __attribute__((aligned(16))) uint16_t rk[RKN];
+    static_assert(SIZE + 256 * 4 + 256 * 2 <= RKN * 2, "rank table must cover occ, cnt and cumul");
     // (no LDS peer masks: the peer-mask ranks run only when an atomic-rank
     // table fails its check, and then match keys by ballot; the 512 B they
     // took kept the kernel at 21 workgroups per CU instead of 22)

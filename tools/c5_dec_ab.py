@@ -17,6 +17,8 @@ n = int(os.environ.get("NB", 256 << 20))
 res = {"lib": os.environ.get("FSEHIP_LIB", "libfsehip.so")}
 for name, kind, prob in (("uni", 2, 0.0), ("skew", 0, 0.77)):
     for L in (12, 13, 14, 15):
+        if os.environ.get("ROWS") and f"{name}{L}" not in os.environ["ROWS"].split(","):
+            continue
         codec = BlockCodec(ckpt_interval=64, table_log=L)
         src = codec.generate(kind, prob, 0x5EED0005, n)
         if L == 15:
