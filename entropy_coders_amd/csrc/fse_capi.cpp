@@ -891,6 +891,18 @@ static void for_streams(size_t n, uint64_t bytes, Fn fn) {
 }
 }  // extern "C++"
 
+// Batches of at most this many streams at table log <= 11 decode one stream
+// per wave on the scalar unit (single_decode_kernel), larger ones on the
+// serial ring kernel (32 lanes of chains per CU).  Measured with 64 KiB C2
+// streams, host buffers in and out (tools/many_ab.py, profiles/r06/many/):
+// 3 streams 2.13 -> 1.48 ms, 16 streams 2.27 -> 2.08 ms (1-state 3.38 ->
+// 2.01), but 64 streams 2.62 -> 2.90: the scalar chains share their CU's
+// scalar cache, whose 16 KiB fused tables then evict one another.
+#ifndef FSE_SCALAR_MANY
+#define FSE_SCALAR_MANY 32
+#endif
+constexpr size_t kScalarMany = FSE_SCALAR_MANY;
+
 // One batch: the streams idx[0..m) (each 0 < n <= kManyStream, non-null),
 // staged at a common stride, decoded as fsehip_decompress_streams does.
 static int decompress_batch(const uint8_t* const* srcs, const size_t* src_lens, const std::vector<size_t>& idx,
@@ -949,6 +961,15 @@ static int decompress_batch(const uint8_t* const* srcs, const size_t* src_lens, 
                                 P.out_len = d_olen;
                                 P.dt = dt;
                                 P.dtinfo = info;
+                                if (mtl == 11u && m <= kScalarMany) {
+                                    // few streams: one scalar-unit chain each (the single
+                                    // call's kernel), ~2x faster per chain than a ring lane
+                                    P.states = static_cast<uint32_t*>(
+                                        lease.get(SCRATCH_STATES, fsehip::single_ftab_bytes() * m, true));
+                                    if (P.states)
+                                        return fsehip::launch_single(P, 11, nullptr) == hipSuccess ? (int)FSE_OK
+                                                                                                    : (int)FSE_ERR_HIP;
+                                }
                                 defer_symbols(lease, P, kern_lmax(mtl));
                                 return fsehip::launch_decode(P, kern_lmax(mtl), nullptr) == hipSuccess
                                            ? (int)FSE_OK

@@ -1805,6 +1805,8 @@ __device__ __forceinline__ void park2(uint32_t& buf, uint32_t a, uint32_t b) {
 // av.  Built per call into DecParams::states (2 words per entry).
 __global__ __launch_bounds__(256) void single_ftab_kernel(const uint32_t* __restrict__ dt, uint32_t* __restrict__ ft,
                                                            uint32_t tw) {
+    dt += (uint64_t)blockIdx.x * tw;  // one workgroup per stream
+    ft += (uint64_t)blockIdx.x * 2u * tw;
     for (uint32_t i = threadIdx.x; i < tw; i += blockDim.x) {
         const uint32_t e = dt[i];
         ft[2u * i] = dte_nb(e) * 0xFFFFu | dte_sym(e) << 24;
@@ -1875,9 +1877,13 @@ template <int NS>
 __global__ __launch_bounds__(64) void single_decode_kernel(DecParams P) {
     constexpr uint32_t LMAX = 11, TW = 1u << LMAX, NV = TW / 64u;
     const uint32_t lane = threadIdx.x;
-    if (blockIdx.x != 0u) return;  // one stream per launch
-    const int32_t info = P.dtinfo[0];
-    const uint32_t clen = P.comp_len[0];
+    // one wave per stream: stream gb at P.in + gb * slot_bytes, its table at
+    // P.dt + gb * 2^11 words, fused at P.states + gb * 2^12 words, its output
+    // at P.out + gb * block_size
+    const uint64_t gb = blockIdx.x;
+    if (gb >= P.n_blocks) return;
+    const int32_t info = P.dtinfo[gb];
+    const uint32_t clen = P.comp_len[gb];
     int32_t err = info < 0 ? info : FSE_OK;
     const uint32_t L = err == FSE_OK ? (uint32_t)info >> 16 : 0u;
     // table into VGPRs; OR of the valid entries' nb: 0 = single-symbol table
@@ -1887,22 +1893,22 @@ __global__ __launch_bounds__(64) void single_decode_kernel(DecParams P) {
         const uint32_t size = 1u << L;
 #pragma unroll
         for (uint32_t k = 0; k < NV; ++k) {
-            vt[k] = P.dt[k * 64u + lane];
+            vt[k] = P.dt[gb * TW + k * 64u + lane];
             if (k * 64u + lane < size) nbor |= vt[k] & 0xFFu;
         }
     }
     const bool single = __ballot(nbor != 0u) == 0ull;
-    uint8_t* out = P.out;
+    uint8_t* out = P.out + gb * P.block_size;
     const uint32_t cap = P.out_cap;
     if (err == FSE_OK && single) err = FSE_ERR_SINGLE_SYMBOL;  // the reference never ends such a stream
     if (err != FSE_OK) {
         if (lane == 0) {
-            P.status[0] = err;
-            if (P.out_len) P.out_len[0] = 0;
+            P.status[gb] = err;
+            if (P.out_len) P.out_len[gb] = 0;
         }
         return;
     }
-    const uint32_t* in32 = reinterpret_cast<const uint32_t*>(P.in);
+    const uint32_t* in32 = reinterpret_cast<const uint32_t*>(P.in + gb * P.slot_bytes);
     const int32_t last = (int32_t)((clen - 1u) >> 2);  // the payload's last word
     // 64 payload words from word c on, one per lane.  Words below word 0 are
     // never consumed (bits below the header are not read), so the index is
@@ -1947,7 +1953,7 @@ __global__ __launch_bounds__(64) void single_decode_kernel(DecParams P) {
         av -= nb;
         return (uint32_t)(W >> av) & ((1u << nb) - 1u);
     };
-    const uint64_t ft = (uint64_t)P.states;
+    const uint64_t ft = (uint64_t)(P.states + gb * 2u * TW);
     uint32_t o = 0;  // bytes decoded
     uint32_t eb = 0;  // the round's 64 entries, one per lane
     auto put64 = [&]() {  // the round's symbols (fused entries: sym in bits 24..31)
@@ -2076,17 +2082,19 @@ __global__ __launch_bounds__(64) void single_decode_kernel(DecParams P) {
         }
     }
     if (lane == 0) {
-        P.status[0] = err;
-        if (P.out_len) P.out_len[0] = err ? 0u : o;
+        P.status[gb] = err;
+        if (P.out_len) P.out_len[gb] = err ? 0u : o;
     }
 }
 
+// P.n_blocks streams, one wave each (P.states: 2^12 words of fused table per stream)
 hipError_t launch_single(const DecParams& P, uint32_t lmax, hipStream_t stream) {
-    if (!P.dt || !P.dtinfo || !P.states || P.n_total || P.sidecar || P.sidecar_out || P.n_blocks != 1 || lmax > 11)
+    if (!P.dt || !P.dtinfo || !P.states || P.n_total || P.sidecar || P.sidecar_out || P.n_blocks == 0 || lmax > 11)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(single_ftab_kernel, dim3(1), dim3(256), 0, stream, P.dt, P.states, 2048u);
-    if (P.nstates == 1) hipLaunchKernelGGL((single_decode_kernel<1>), dim3(1), dim3(64), 0, stream, P);
-    else hipLaunchKernelGGL((single_decode_kernel<2>), dim3(1), dim3(64), 0, stream, P);
+    const dim3 g(P.n_blocks);
+    hipLaunchKernelGGL(single_ftab_kernel, g, dim3(256), 0, stream, P.dt, P.states, 2048u);
+    if (P.nstates == 1) hipLaunchKernelGGL((single_decode_kernel<1>), g, dim3(64), 0, stream, P);
+    else hipLaunchKernelGGL((single_decode_kernel<2>), g, dim3(64), 0, stream, P);
     return hipGetLastError();
 }
 

@@ -100,7 +100,9 @@ int fse_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, s
  * 4,000 (14.8 GiB/s), PCIe included, so it beats one host core from ~16
  * streams and 16 cores from ~256 (tools/many_streams.py; bench.py's
  * host_call_latency reports 1,000 streams).  One or two streams take the
- * single-stream path.  Synchronous on the default stream; the
+ * single-stream path; batches of up to 32 streams at table log <= 11 run
+ * the single-stream kernel once per stream in one launch (3 streams 1.5 ms,
+ * 16 streams 2.1 ms; 1-state 16 streams 2.0 ms, tools/many_ab.py).  Synchronous on the default stream; the
  * staging buffers are per thread (grow-only, freed by
  * fsehip_release_workspace). */
 int fse_decompress2_many(const uint8_t* const* srcs, const size_t* src_lens, size_t n_streams, uint8_t* dst,

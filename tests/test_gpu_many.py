@@ -80,6 +80,39 @@ def test_many_streams_exact(torch_cuda, nstates):
     assert n_ok >= 950 and n_err >= 1 and n_ok + n_err == len(streams) - 1, (n_ok, n_err)
 
 
+@pytest.mark.parametrize("nstates", [2, 1])
+@pytest.mark.parametrize("m", [3, 17, 32, 33])
+def test_many_streams_scalar_batches(torch_cuda, nstates, m):
+    """Batches of up to 32 streams at table log <= 11 run one scalar-unit
+    chain per stream (single_decode_kernel over the batch), larger ones the
+    ring kernel: both sides of that boundary, with damaged, truncated,
+    ragged and empty streams and short strides, against the oracle."""
+    from entropy_coders_amd import decompress2_many
+
+    rng = np.random.default_rng(0x5CA1 + 7 * m + nstates)
+    streams = _streams(rng, 3 * m, nstates)
+    # keep m (the EMPTY one last), with a damaged and a truncated one among them
+    streams = streams[: m - 1] + [streams[-1]]
+    streams[1] = bytes(bytearray(streams[1])[: max(1, len(streams[1]) // 2)])
+    if m > 3:  # (index m - 1 is the empty stream)
+        b = bytearray(streams[2])
+        b[len(b) // 2] ^= 0x55
+        streams[2] = bytes(b)
+    ref = O.decompress2 if nstates == 2 else O.decompress
+    for stride in (65536, 30000):
+        got = decompress2_many(streams, stride, nstates=nstates)
+        for i, (x, g) in enumerate(zip(streams, got)):
+            if not x:
+                assert g == "EMPTY", (i, g)
+                continue
+            try:
+                want = ref(x, stride)
+            except O.OracleError as e:
+                assert g == e.code, (m, stride, i, e.code, g)
+                continue
+            assert g == want, (m, stride, i)
+
+
 def test_many_streams_short_stride_and_small_batches(torch_cuda):
     """DST_TOO_SMALL per stream when the stride is short, and the one- and
     two-stream batches (which take the single-stream path) agree with the
