@@ -102,9 +102,9 @@ int fse_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap, s
  * host_call_latency reports 1,000 streams).  One or two streams take the
  * single-stream path; batches of up to 32 streams at table log <= 11 run
  * the single-stream kernel once per stream in one launch (3 streams 1.5 ms,
- * 16 streams 2.1 ms; 1-state 16 streams 2.0 ms, tools/many_ab.py).  Synchronous on the default stream; the
- * staging buffers are per thread (grow-only, freed by
- * fsehip_release_workspace). */
+ * 16 streams 2.1 ms; 1-state 16 streams 2.0 ms, tools/many_ab.py).
+ * Synchronous on the default stream; the staging buffers are per thread
+ * (grow-only, freed by fsehip_release_workspace). */
 int fse_decompress2_many(const uint8_t* const* srcs, const size_t* src_lens, size_t n_streams, uint8_t* dst,
                          size_t dst_stride, size_t* dst_lens, int32_t* statuses);
 int fse_decompress_many(const uint8_t* const* srcs, const size_t* src_lens, size_t n_streams, uint8_t* dst,
